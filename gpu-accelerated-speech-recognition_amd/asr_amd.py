@@ -1,0 +1,381 @@
+"""Python host mirror of the reference's C++ API over libasr_amd.so (ctypes).
+
+The reference (jrxk/GPU-Accelerated-Speech-Recognition) exposes C++ classes
+only; its callers are main.cpp / nn_test.cpp.  This module mirrors those
+classes for Python callers, tests and bench.py, calling the C ABI of
+include/asr_amd.h — it contains no arithmetic of its own:
+
+    CTCBeamSearch(vocab, vocabSize, beamWidth, blankID)   CTCBeamSearch.h:107
+        .decode(seqProb, timestep, batchSize)             CTCBeamSearch.cu:262
+    Linear(batch_size, input_size, output_size).forward   Linear.cu:42
+    RNN_Cell(batch, in, hidden).forward                   RNN_Cell.cu:65
+    RNN(batch, in, hidden, time_step, num_layers).forward RNN.cu:9
+    DeviceMatrix ~ cuMatrix<float> (toGpu / toCpu)        cuMatrix.h:72-105
+
+The native library is required: importing this module on a machine where
+libasr_amd.so is missing raises, there is no fallback path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libasr_amd.so"
+
+ASR_OK = 0
+ASR_ERR_ARG = 1
+ASR_ERR_HIP = 2
+ASR_ERR_OOM = 3
+ASR_ERR_BEAM_OVERFLOW = 4
+ASR_ERR_UNSUPPORTED = 5
+ASR_ERR_STATE = 6
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_LOGSOFTMAX = 0, 1, 2, 3
+
+# Every symbol include/asr_amd.h declares (checked by tests/test_boundary.py).
+EXPORTS = [
+    "asr_status_string", "asr_version", "asr_get_device_count", "asr_set_device",
+    "asr_get_device", "asr_device_malloc", "asr_device_free", "asr_host_malloc",
+    "asr_host_free", "asr_memcpy_h2d", "asr_memcpy_d2h", "asr_memcpy_d2d", "asr_memset",
+    "asr_stream_create", "asr_stream_destroy", "asr_stream_sync", "asr_device_sync",
+    "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
+    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
+    "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
+    "asr_ctc_get_config",
+]
+
+
+class AsrError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {status_string(status)} (status {status})")
+
+
+_lib: Optional[ctypes.CDLL] = None
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_sz = ctypes.c_size_t
+_f = ctypes.c_float
+
+
+def lib() -> ctypes.CDLL:
+    """Load libasr_amd.so (built by `make` in this directory)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"{LIB_PATH} not found: build it with __graft_entry__.build() "
+                           "or `make -C gpu-accelerated-speech-recognition_amd`")
+    L = ctypes.CDLL(str(LIB_PATH))
+    L.asr_status_string.restype = ctypes.c_char_p
+    L.asr_status_string.argtypes = [_i]
+    L.asr_version.restype = ctypes.c_char_p
+    sig = {
+        "asr_get_device_count": [ctypes.POINTER(_i)],
+        "asr_set_device": [_i],
+        "asr_get_device": [ctypes.POINTER(_i)],
+        "asr_device_malloc": [ctypes.POINTER(_vp), _sz],
+        "asr_device_free": [_vp],
+        "asr_host_malloc": [ctypes.POINTER(_vp), _sz],
+        "asr_host_free": [_vp],
+        "asr_memcpy_h2d": [_vp, _vp, _sz, _vp],
+        "asr_memcpy_d2h": [_vp, _vp, _sz, _vp],
+        "asr_memcpy_d2d": [_vp, _vp, _sz, _vp],
+        "asr_memset": [_vp, _i, _sz, _vp],
+        "asr_stream_create": [ctypes.POINTER(_vp)],
+        "asr_stream_destroy": [_vp],
+        "asr_stream_sync": [_vp],
+        "asr_device_sync": [],
+        "asr_matmul": [_vp, _vp, _vp, _i, _i, _i, _vp],
+        "asr_matmul_ta": [_vp, _vp, _vp, _i, _i, _i, _vp],
+        "asr_matmul_tb": [_vp, _vp, _vp, _i, _i, _i, _vp],
+        "asr_matadd": [_vp, _vp, _vp, _i, _i, _f, _vp],
+        "asr_linear_fwd": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
+        "asr_rnn_cell_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
+        "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
+        "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
+        "asr_ctc_destroy": [_vp],
+        "asr_ctc_decode": [_vp, _vp, _i, _i, _i, _vp],
+        "asr_ctc_get_best": [_vp, _vp, _i, _vp, _vp],
+        "asr_ctc_get_beams": [_vp, _i, _i, _vp, _vp, _vp, _vp],
+        "asr_ctc_last_kernel_ms": [_vp, ctypes.POINTER(_f)],
+        "asr_ctc_set_waves": [_vp, _i],
+        "asr_ctc_get_config": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = _i
+    _lib = L
+    return L
+
+
+def status_string(status: int) -> str:
+    return lib().asr_status_string(status).decode()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != ASR_OK:
+        raise AsrError(rc, what)
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = _i(0)
+    check(lib().asr_get_device_count(ctypes.byref(n)), "asr_get_device_count")
+    return n.value
+
+
+def set_device(d: int) -> None:
+    check(lib().asr_set_device(d), "asr_set_device")
+
+
+def synchronize() -> None:
+    check(lib().asr_device_sync(), "asr_device_sync")
+
+
+class DeviceMatrix:
+    """fp32 row-major device buffer (cuMatrix<float> device side)."""
+
+    def __init__(self, rows: int, cols: int = 1, data: Optional[np.ndarray] = None):
+        self.rows, self.cols = int(rows), int(cols)
+        self.nbytes = 4 * self.rows * self.cols
+        p = _vp()
+        check(lib().asr_device_malloc(ctypes.byref(p), self.nbytes), "asr_device_malloc")
+        self.ptr = p.value or 0
+        if data is not None:
+            self.toGpu(data)
+
+    @classmethod
+    def from_numpy(cls, a: np.ndarray) -> "DeviceMatrix":
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        r = a.shape[0] if a.ndim else 1
+        return cls(r, a.size // max(r, 1), a)
+
+    def toGpu(self, a: np.ndarray, stream: int = 0) -> None:
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        assert a.size * 4 == self.nbytes, (a.shape, self.rows, self.cols)
+        check(lib().asr_memcpy_h2d(self.ptr, _ptr(a), self.nbytes, stream), "asr_memcpy_h2d")
+
+    def toCpu(self, stream: int = 0) -> np.ndarray:
+        out = np.empty((self.rows, self.cols), dtype=np.float32)
+        check(lib().asr_memcpy_d2h(_ptr(out), self.ptr, self.nbytes, stream), "asr_memcpy_d2h")
+        return out
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().asr_device_free(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceBytes:
+    """Untyped device allocation (workspace / generic buffers)."""
+
+    def __init__(self, nbytes: int):
+        p = _vp()
+        check(lib().asr_device_malloc(ctypes.byref(p), int(nbytes)), "asr_device_malloc")
+        self.ptr, self.nbytes = p.value or 0, int(nbytes)
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().asr_device_free(self.ptr)
+        except Exception:
+            pass
+
+
+# --------------------------------------------------------------------- dense
+def linear_fwd(x: DeviceMatrix, W: DeviceMatrix, b: Optional[DeviceMatrix], y: DeviceMatrix,
+               epilogue: int = EPI_BIAS_RELU, stream: int = 0) -> DeviceMatrix:
+    M, K = x.rows, x.cols
+    N = W.cols
+    assert W.rows == K and y.rows == M and y.cols == N
+    check(lib().asr_linear_fwd(x.ptr, W.ptr, b.ptr if b else None, y.ptr, M, K, N, epilogue,
+                               stream), "asr_linear_fwd")
+    return y
+
+
+def rnn_fwd(x: DeviceMatrix, W_ih: DeviceMatrix, W_hh: DeviceMatrix, b_ih: DeviceMatrix,
+            b_hh: DeviceMatrix, hid: DeviceMatrix, T: int, B: int,
+            h0: Optional[DeviceMatrix] = None, stream: int = 0) -> DeviceMatrix:
+    inp, H = W_ih.rows, W_ih.cols
+    check(lib().asr_rnn_fwd(x.ptr, h0.ptr if h0 else None, W_ih.ptr, W_hh.ptr, b_ih.ptr,
+                            b_hh.ptr, hid.ptr, T, B, inp, H, stream), "asr_rnn_fwd")
+    return hid
+
+
+def rnn_cell_fwd(x: DeviceMatrix, h_prev: DeviceMatrix, W_ih: DeviceMatrix,
+                 W_hh: DeviceMatrix, b_ih: DeviceMatrix, b_hh: DeviceMatrix,
+                 h_out: DeviceMatrix, stream: int = 0) -> DeviceMatrix:
+    B, inp = x.rows, x.cols
+    H = W_ih.cols
+    check(lib().asr_rnn_cell_fwd(x.ptr, h_prev.ptr, W_ih.ptr, W_hh.ptr, b_ih.ptr, b_hh.ptr,
+                                 h_out.ptr, B, inp, H, stream), "asr_rnn_cell_fwd")
+    return h_out
+
+
+class Linear:
+    """Linear.h: y = relu(x.W + b), W [in, out] row-major (Linear.cu:42-49)."""
+
+    def __init__(self, batch_size: int, input_size: int, output_size: int,
+                 weight: Optional[np.ndarray] = None, bias: Optional[np.ndarray] = None,
+                 epilogue: int = EPI_BIAS_RELU):
+        self.batch_size, self.input_size, self.output_size = batch_size, input_size, output_size
+        w = np.zeros((input_size, output_size), np.float32) if weight is None else weight
+        b = np.zeros((output_size,), np.float32) if bias is None else bias
+        self.w = DeviceMatrix.from_numpy(np.asarray(w, np.float32).reshape(input_size, output_size))
+        self.b = DeviceMatrix.from_numpy(np.asarray(b, np.float32).reshape(output_size, 1))
+        self.outputs = DeviceMatrix(batch_size, output_size)
+        self.epilogue = epilogue
+
+    def forward(self, inputs: DeviceMatrix, stream: int = 0) -> DeviceMatrix:
+        return linear_fwd(inputs, self.w, self.b, self.outputs, self.epilogue, stream)
+
+
+class RNN:
+    """RNN.h: tanh RNN, num_layers stacked, time-major [T*B, H] hiddens."""
+
+    def __init__(self, batch_size: int, input_size: int, hidden_size: int, time_step: int,
+                 num_layers: int = 1, params: Optional[Sequence[Tuple[np.ndarray, ...]]] = None):
+        self.B, self.inp, self.H, self.T, self.L = batch_size, input_size, hidden_size, time_step, num_layers
+        self.layers = []
+        for l in range(num_layers):
+            i = input_size if l == 0 else hidden_size
+            if params is None:
+                p = (np.zeros((i, hidden_size), np.float32), np.zeros((hidden_size, hidden_size), np.float32),
+                     np.zeros(hidden_size, np.float32), np.zeros(hidden_size, np.float32))
+            else:
+                p = params[l]
+            w_ih, w_hh, b_ih, b_hh = (DeviceMatrix.from_numpy(np.asarray(a, np.float32).reshape(
+                (i, hidden_size) if k == 0 else (hidden_size, hidden_size) if k == 1 else (hidden_size, 1)))
+                for k, a in enumerate(p))
+            self.layers.append((w_ih, w_hh, b_ih, b_hh))
+        self.hiddens = [DeviceMatrix(time_step * batch_size, hidden_size) for _ in range(num_layers)]
+
+    def forward(self, inputs: DeviceMatrix, stream: int = 0) -> DeviceMatrix:
+        x = inputs
+        for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(self.layers):
+            rnn_fwd(x, w_ih, w_hh, b_ih, b_hh, self.hiddens[l], self.T, self.B, None, stream)
+            x = self.hiddens[l]
+        return self.hiddens[-1]
+
+
+# ----------------------------------------------------------------------- CTC
+class CTCDecoder:
+    """Handle over asr_ctc_*: decode time-major emissions [T][B][V]."""
+
+    def __init__(self, V: int, beam_width: int, blank_id: int = 0,
+                 codes: Optional[Sequence[int]] = None, max_states: int = 0, waves: int = 0):
+        self.V, self.beam, self.blank = V, beam_width, blank_id
+        self.codes = None if codes is None else np.ascontiguousarray(codes, dtype=np.int32)
+        h = _vp()
+        check(lib().asr_ctc_create(_ptr(self.codes) if self.codes is not None else None, V,
+                                   beam_width, blank_id, max_states, ctypes.byref(h)),
+              "asr_ctc_create")
+        self.h = h.value
+        if waves:
+            check(lib().asr_ctc_set_waves(self.h, waves), "asr_ctc_set_waves")
+        self._emis: Optional[DeviceBytes] = None
+        self.T = self.B = 0
+
+    def config(self) -> Tuple[int, int, int]:
+        ms, w, lds = _i(), _i(), _i()
+        check(lib().asr_ctc_get_config(self.h, ctypes.byref(ms), ctypes.byref(w), ctypes.byref(lds)),
+              "asr_ctc_get_config")
+        return ms.value, w.value, lds.value
+
+    def set_waves(self, waves: int) -> None:
+        check(lib().asr_ctc_set_waves(self.h, waves), "asr_ctc_set_waves")
+
+    def decode_device(self, d_emis: int, T: int, B: int, is_log: bool, stream: int = 0) -> None:
+        check(lib().asr_ctc_decode(self.h, d_emis, T, B, int(bool(is_log)), stream), "asr_ctc_decode")
+        self.T, self.B = T, B
+
+    def decode(self, emis: np.ndarray, is_log: bool = False, stream: int = 0) -> None:
+        """Upload emis [T][B][V] (fp32) and enqueue the decode."""
+        emis = np.ascontiguousarray(emis, dtype=np.float32)
+        T, B, V = emis.shape
+        assert V == self.V, (V, self.V)
+        if self._emis is None or self._emis.nbytes < emis.nbytes:
+            self._emis = DeviceBytes(emis.nbytes)
+        check(lib().asr_memcpy_h2d(self._emis.ptr, _ptr(emis), emis.nbytes, stream), "asr_memcpy_h2d")
+        self.decode_device(self._emis.ptr, T, B, is_log, stream)
+
+    def best(self, allow_overflow: bool = False) -> Tuple[List[List[int]], np.ndarray]:
+        """Best label sequence and fp64 log-prob of every utterance."""
+        B, T = self.B, self.T
+        lab = np.zeros((B, T), np.int32)
+        ln = np.zeros(B, np.int32)
+        lp = np.zeros(B, np.float64)
+        rc = lib().asr_ctc_get_best(self.h, _ptr(lab), T, _ptr(ln), _ptr(lp))
+        if not (allow_overflow and rc == ASR_ERR_BEAM_OVERFLOW):
+            check(rc, "asr_ctc_get_best")
+        return [list(lab[b, :ln[b]]) for b in range(B)], lp
+
+    def beams(self, max_hyps: int) -> List[List[Tuple[List[int], float]]]:
+        """Ranked final beam (logp desc, string asc) of every utterance."""
+        B, T = self.B, self.T
+        nh = np.zeros(B, np.int32)
+        ln = np.zeros((B, max_hyps), np.int32)
+        lab = np.zeros((B, max_hyps, max(T, 1)), np.int32)
+        lp = np.zeros((B, max_hyps), np.float64)
+        check(lib().asr_ctc_get_beams(self.h, max_hyps, max(T, 1), _ptr(nh), _ptr(ln), _ptr(lab),
+                                      _ptr(lp)), "asr_ctc_get_beams")
+        return [[(list(lab[b, k, :ln[b, k]]), float(lp[b, k])) for k in range(min(nh[b], max_hyps))]
+                for b in range(B)]
+
+    def last_kernel_ms(self) -> float:
+        ms = _f()
+        check(lib().asr_ctc_last_kernel_ms(self.h, ctypes.byref(ms)), "asr_ctc_last_kernel_ms")
+        return ms.value
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().asr_ctc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CTCBeamSearch:
+    """CTCBeamSearch.h:107 — CTCBeamSearch(vocab, vocabSize, beamWidth, blankID).
+
+    decode(seqProb, timestep, batchSize) takes probabilities [T*B, V]
+    (time-major rows, CTCBeamSearch.cu:67-69) and returns, per utterance, the
+    best string and its probability as float (cu:283-298); `logprobs` holds
+    the fp64 log-probabilities of the last decode.
+    """
+
+    def __init__(self, vocab: Sequence[str], vocabSize: int, beamWidth: int, blankID: int):
+        self.vocab = [str(c) for c in list(vocab)[:vocabSize]]
+        self.vocabSize, self.beamWidth, self.blankID = vocabSize, beamWidth, blankID
+        codes = [ord(c) & 0xFF if len(c) == 1 else i for i, c in enumerate(self.vocab)]
+        self._dec = CTCDecoder(vocabSize, beamWidth, blankID, codes)
+        self.logprobs: Optional[np.ndarray] = None
+
+    def decode(self, seqProb: np.ndarray, timestep: int, batchSize: int) -> List[Tuple[str, float]]:
+        seqProb = np.asarray(seqProb, np.float32)
+        if seqProb.shape[-1] != self.vocabSize:
+            raise ValueError("Error: inconsistent vocabulary size in CTC decoder")
+        self._dec.decode(seqProb.reshape(timestep, batchSize, self.vocabSize), is_log=False)
+        labels, lp = self._dec.best()
+        self.logprobs = lp
+        return [("".join(self.vocab[i] for i in lab), float(np.exp(l))) for lab, l in zip(labels, lp)]

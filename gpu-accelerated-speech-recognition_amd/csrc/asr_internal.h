@@ -1,0 +1,43 @@
+// Internal declarations shared by the HIP translation units of libasr_amd.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "asr_amd.h"
+
+#define ASR_HIP_TRY(expr)                                                        \
+    do {                                                                         \
+        hipError_t e_ = (expr);                                                  \
+        if (e_ != hipSuccess) {                                                  \
+            asr_internal_set_error(#expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return e_ == hipErrorOutOfMemory ? ASR_ERR_OOM : ASR_ERR_HIP;        \
+        }                                                                        \
+    } while (0)
+
+#define ASR_LAUNCH_TRY()                                                         \
+    do {                                                                         \
+        hipError_t e_ = hipGetLastError();                                       \
+        if (e_ != hipSuccess) {                                                  \
+            asr_internal_set_error("kernel launch", hipGetErrorString(e_), __FILE__, __LINE__); \
+            return ASR_ERR_HIP;                                                  \
+        }                                                                        \
+    } while (0)
+
+void asr_internal_set_error(const char* what, const char* msg, const char* file, int line);
+
+static inline hipStream_t asr_stream(asr_stream_t s) { return (hipStream_t)s; }
+
+// Order-preserving bijection fp64 <-> u64: a < b  <=>  key(a) < key(b).
+// -0.0 is folded onto +0.0 (they compare equal as doubles).  Key 0 is never
+// produced for a non-NaN value (-inf maps to 0x000FFFFFFFFFFFFF), so it marks
+// an absent candidate.
+__host__ __device__ static inline uint64_t asr_d2key(double x) {
+    x = x + 0.0;
+    uint64_t u = __builtin_bit_cast(uint64_t, x);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__host__ __device__ static inline double asr_key2d(uint64_t k) {
+    uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __builtin_bit_cast(double, u);
+}

@@ -1,0 +1,40 @@
+// Host/device interface of the CTC beam-search kernels (ctc_beam.hip).
+#pragma once
+#include "asr_internal.h"
+
+namespace asr {
+
+// Launch geometry of one decode, shared by the host planner and the kernel.
+struct CtcGeom {
+    int V;       // labels incl. blank (<= 63)
+    int blank;   // blank label id
+    int K;       // beamWidth + 1 states kept (cpp:107 cutoff index)
+    int kcap;    // slot/state capacity incl. ties at the cutoff
+    int sb;      // log2 of the candidate row stride (row = V+1 columns)
+    int ch;      // emission frames staged per prefetch chunk
+    int ht;      // hash-table cells (power of two >= 2*kcap)
+};
+
+struct CtcArgs {
+    CtcGeom g;
+    const float* emis;      // [T][B][V]
+    int T, B;
+    int is_log;
+    uint64_t blank_less;    // bit c: code(blank) < code(c)
+    int2* nodes;            // [B][T*kcap] (parent node, label)
+    int* fin_n;             // [B] final hypotheses
+    int* fin_node;          // [B][kcap]
+    double* fin_score;      // [B][kcap]
+    int* status;            // [B] 1 = beam overflow
+    int* best_lab;          // [B][T] reversed labels of the best hypothesis
+    int* best_len;          // [B]
+    double* best_score;     // [B]
+};
+
+size_t ctc_lds_bytes(const CtcGeom& g);
+int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
+int ctc_launch_best(const CtcArgs& a, const int* d_codes, hipStream_t s);
+int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);
+int ctc_set_max_lds();
+
+}  // namespace asr

@@ -1,0 +1,35 @@
+// Host/device interface of the dense fp32 kernels (dense.hip).
+#pragma once
+#include "asr_internal.h"
+
+namespace asr {
+
+enum GemmEpilogue {
+    EPI_NONE = 0,        // C = A.B
+    EPI_BIAS = 1,        // C = A.B + b1
+    EPI_BIAS_RELU = 2,   // C = max(A.B + b1, 0)
+    EPI_LOGSOFTMAX = 3,  // C = log_softmax(A.B + b1) per row, N <= 64
+    EPI_DUAL_TANH = 4,   // C = tanh((A.B + A2.B2) + (b2 + b1))
+    EPI_ADD_TANH = 5     // C = tanh((D + A.B) + (b2 + b1)); C may alias D
+};
+
+struct GemmArgs {
+    const float* A;   // A(m,k) = A[m*sam + k*sak]
+    const float* B;   // B(k,n) = B[k*sbk + n*sbn]
+    const float* A2;  // EPI_DUAL_TANH: [M][K2] row-major
+    const float* B2;  // EPI_DUAL_TANH: [K2][N] row-major
+    const float* b1;
+    const float* b2;
+    const float* D;   // EPI_ADD_TANH addend, [M][ldc]
+    float* C;         // [M][ldc]
+    int M, N, K, K2;
+    long sam, sak, sbk, sbn, ldc;
+};
+
+int gemm_launch(const GemmArgs& g, int epi, hipStream_t s);
+int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
+                     float* hid, int T, int B, int H, hipStream_t s);
+int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
+int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
+
+}  // namespace asr

@@ -1,0 +1,324 @@
+// ============================================================================
+// Dense fp32 ops of the RNN acoustic model on gfx950:
+//  * an LDS-tiled GEMM on v_mfma_f32_16x16x4_f32 (exact fp32, no TF32 on
+//    CDNA4) with fused epilogues — replaces cublasSgemm + the ReLU / Tanh
+//    kernels of the reference (cuMatrix.cpp:33-70, Linear.cu:3-10,
+//    RNN_Cell.cu:5-13);
+//  * a persistent RNN recurrence that keeps W_hh in registers for the whole
+//    sequence (H <= 256), one workgroup per utterance (RNN.cu:9-30 ran
+//    2 GEMMs + a GEAM + a kernel + 3 host syncs per step);
+//  * z = x + lambda*y (matrixAdd, cuMatrix.cpp:147-168).
+// ============================================================================
+#include "dense.h"
+
+namespace asr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 64;   // rows per workgroup: 4 waves x 16 rows
+constexpr int BK = 16;   // k per LDS stage
+constexpr int AST = BK + 2;   // As row stride (floats): conflict-free A-fragment reads
+
+template <int BN>
+struct Tile {
+    static constexpr int BST = BN + 16;   // Bs row stride: k and k+1 land 16 banks apart
+    float As[BM * AST];
+    float Bs[BK * BST];
+};
+
+// Accumulate A[M,K] . B[K,N] for this workgroup's 64 x BN tile into acc[].
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn].  VEC: sak == 1 and
+// sbn == 1 with 16-byte aligned rows, loaded as float4.
+template <int BN, bool VEC>
+__device__ __forceinline__ void mma_tile(Tile<BN>& L, const float* __restrict__ A,
+                                         const float* __restrict__ Bm, int M, int N, int K,
+                                         long sam, long sak, long sbk, long sbn, int m0, int n0,
+                                         f32x4 (&acc)[BN / 16]) {
+    constexpr int BST = Tile<BN>::BST;
+    constexpr int NB4 = BN / 4;                 // float4 per B row
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ar = tid >> 2, ak = (tid & 3) * 4;            // A: 64 rows x 4 float4
+    const int bkr = tid / NB4, bn = (tid % NB4) * 4;        // B: 16 rows x NB4 float4
+    const bool bact = tid < BK * NB4;
+    float ra[4], rb[4];
+
+    auto load = [&](int k0) {
+        const int gm = m0 + ar, gk = k0 + ak;
+        if (VEC && gm < M && gk + 3 < K) {
+            const float4 v = *reinterpret_cast<const float4*>(A + gm * sam + gk);
+            ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                ra[i] = (gm < M && gk + i < K) ? A[gm * sam + (long)(gk + i) * sak] : 0.f;
+        }
+        const int gkb = k0 + bkr, gn = n0 + bn;
+        if (bact) {
+            if (VEC && gkb < K && gn + 3 < N) {
+                const float4 v = *reinterpret_cast<const float4*>(Bm + gkb * sbk + gn);
+                rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    rb[i] = (gkb < K && gn + i < N) ? Bm[gkb * sbk + (long)(gn + i) * sbn] : 0.f;
+            }
+        }
+    };
+
+    load(0);
+    for (int k0 = 0; k0 < K; k0 += BK) {
+        __syncthreads();   // previous stage fully consumed
+#pragma unroll
+        for (int i = 0; i < 4; i++) L.As[ar * AST + ak + i] = ra[i];
+        if (bact) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) L.Bs[bkr * BST + bn + i] = rb[i];
+        }
+        __syncthreads();
+        if (k0 + BK < K) load(k0 + BK);   // next stage in flight during the MFMAs
+#pragma unroll
+        for (int kk = 0; kk < BK / 4; kk++) {
+            const float af = L.As[(w * 16 + (lane & 15)) * AST + kk * 4 + (lane >> 4)];
+#pragma unroll
+            for (int nt = 0; nt < BN / 16; nt++) {
+                const float bf = L.Bs[(kk * 4 + (lane >> 4)) * BST + nt * 16 + (lane & 15)];
+                acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, bf, acc[nt], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// C/D layout of 16x16 MFMA tiles (dtype-independent on gfx950):
+// element j of lane l is row (l>>4)*4 + j, column l & 15.
+template <int BN, int EPI, bool VEC>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+    __shared__ Tile<BN> L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    f32x4 acc[BN / 16], acc2[BN / 16];
+#pragma unroll
+    for (int nt = 0; nt < BN / 16; nt++) {
+        acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    mma_tile<BN, VEC>(L, g.A, g.B, g.M, g.N, g.K, g.sam, g.sak, g.sbk, g.sbn, m0, n0, acc);
+    if (EPI == EPI_DUAL_TANH)
+        mma_tile<BN, VEC>(L, g.A2, g.B2, g.M, g.N, g.K2, g.K2, 1, g.N, 1, m0, n0, acc2);
+
+    const int rbase = m0 + w * 16 + (lane >> 4) * 4;
+    if (EPI == EPI_LOGSOFTMAX) {
+        // Whole row in this workgroup (N <= BN): row r = rbase + j lives in
+        // the 16 lanes of group lane>>4, across the BN/16 tiles.
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            float v[BN / 16];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int nt = 0; nt < BN / 16; nt++) {
+                const int col = n0 + nt * 16 + (lane & 15);
+                v[nt] = col < g.N ? acc[nt][j] + g.b1[col] : -INFINITY;
+                mx = fmaxf(mx, v[nt]);
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            float s = 0.f;
+#pragma unroll
+            for (int nt = 0; nt < BN / 16; nt++) s += expf(v[nt] - mx);
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);
+            const float lz = mx + logf(s);
+            const int row = rbase + j;
+            if (row < g.M) {
+#pragma unroll
+                for (int nt = 0; nt < BN / 16; nt++) {
+                    const int col = n0 + nt * 16 + (lane & 15);
+                    if (col < g.N) g.C[(long)row * g.ldc + col] = v[nt] - lz;
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int nt = 0; nt < BN / 16; nt++) {
+        const int col = n0 + nt * 16 + (lane & 15);
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int row = rbase + j;
+            if (row >= g.M) continue;
+            float y = acc[nt][j];
+            if (EPI == EPI_BIAS) {
+                y = y + g.b1[col];
+            } else if (EPI == EPI_BIAS_RELU) {   // Linear.cu:8-9
+                y = y + g.b1[col];
+                if (y < 0.f) y = 0.f;
+            } else if (EPI == EPI_DUAL_TANH) {   // RNN_Cell.cu:10-12: (ih + hh) + (b_hh + b_ih)
+                y = tanhf((y + acc2[nt][j]) + (g.b2[col] + g.b1[col]));
+            } else if (EPI == EPI_ADD_TANH) {    // D holds x.W_ih for this step
+                y = tanhf((g.D[(long)row * g.ldc + col] + y) + (g.b2[col] + g.b1[col]));
+            }
+            g.C[(long)row * g.ldc + col] = y;
+        }
+    }
+}
+
+template <int BN, int EPI>
+static int launch_gemm_bn(const GemmArgs& g, hipStream_t s) {
+    const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
+    bool vec = g.sak == 1 && g.sbn == 1 && (g.K % 4) == 0 && (g.N % 4) == 0 &&
+               ((uintptr_t)g.A % 16) == 0 && ((uintptr_t)g.B % 16) == 0;
+    if (EPI == EPI_DUAL_TANH)
+        vec = vec && (g.K2 % 4) == 0 && ((uintptr_t)g.A2 % 16) == 0 && ((uintptr_t)g.B2 % 16) == 0;
+    if (vec) hipLaunchKernelGGL((gemm_kernel<BN, EPI, true>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_kernel<BN, EPI, false>), grid, dim3(256), 0, s, g);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+template <int EPI>
+static int launch_gemm_epi(const GemmArgs& g, hipStream_t s) {
+    if (g.N <= 32) return launch_gemm_bn<32, EPI>(g, s);
+    return launch_gemm_bn<64, EPI>(g, s);
+}
+
+int gemm_launch(const GemmArgs& g, int epi, hipStream_t s) {
+    if (g.M <= 0 || g.N <= 0 || g.K <= 0) return ASR_ERR_ARG;
+    if (epi == EPI_LOGSOFTMAX && g.N > 64) return ASR_ERR_UNSUPPORTED;
+    switch (epi) {
+        case EPI_NONE: return launch_gemm_epi<EPI_NONE>(g, s);
+        case EPI_BIAS: return launch_gemm_epi<EPI_BIAS>(g, s);
+        case EPI_BIAS_RELU: return launch_gemm_epi<EPI_BIAS_RELU>(g, s);
+        case EPI_LOGSOFTMAX: return launch_gemm_epi<EPI_LOGSOFTMAX>(g, s);
+        case EPI_DUAL_TANH: return launch_gemm_epi<EPI_DUAL_TANH>(g, s);
+        case EPI_ADD_TANH: return launch_gemm_epi<EPI_ADD_TANH>(g, s);
+        default: return ASR_ERR_ARG;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// RNN recurrence, H <= 256: h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih))
+// where P = x.W_ih was produced for all T by one GEMM into `hid`, which is
+// overwritten in place by h.  One 1024-thread workgroup per utterance; thread
+// (j, q) holds column j of W_hh for k in quarter q (64 registers), so W_hh is
+// read from HBM once per utterance instead of once per step.  h_{t-1} is
+// broadcast from LDS as [quarter][68] (conflict-free ds_read_b128).
+// ---------------------------------------------------------------------------
+constexpr int RNN_HMAX = 256;
+constexpr int RNN_QS = 68;   // LDS stride of one quarter (floats)
+
+__global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict__ h0,
+                                                         const float* __restrict__ Whh,
+                                                         const float* __restrict__ b_ih,
+                                                         const float* __restrict__ b_hh,
+                                                         float* __restrict__ hid, int T, int B,
+                                                         int H) {
+    __shared__ __attribute__((aligned(16))) float hs[2][4 * RNN_QS];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int j = tid >> 2, q = tid & 3;
+    const int KQ = (H + 3) >> 2;            // k per quarter
+    const bool col = j < H;
+    float w[64];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        const int k = q * KQ + i;
+        w[i] = (col && i < KQ && k < H) ? Whh[(long)k * H + j] : 0.f;
+    }
+    for (int i = tid; i < 2 * 4 * RNN_QS; i += 1024) (&hs[0][0])[i] = 0.f;
+    __syncthreads();
+    if (tid < H) {
+        const int qq = tid / KQ, ii = tid - qq * KQ;
+        hs[0][qq * RNN_QS + ii] = h0 ? h0[(long)b * H + tid] : 0.f;
+    }
+    const float bias = col ? (b_hh[j] + b_ih[j]) : 0.f;
+    const int jq = col ? j / KQ : 0, ji = col ? j - jq * KQ : 0;
+    const bool writer = col && q == 0;
+    float* prow = hid + (long)b * H + j;     // P_t / h_t at prow[t*B*H]
+    const long tstride = (long)B * H;
+    float pnext = writer ? prow[0] : 0.f;
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < T; t++) {
+        const float p = pnext;
+        if (writer && t + 1 < T) pnext = prow[(t + 1) * tstride];
+        const float4* hq = reinterpret_cast<const float4*>(&hs[cur][q * RNN_QS]);
+        float acc = 0.f;
+#pragma unroll
+        for (int i4 = 0; i4 < 16; i4++) {
+            const float4 h4 = hq[i4];
+            acc = fmaf(h4.x, w[4 * i4 + 0], acc);
+            acc = fmaf(h4.y, w[4 * i4 + 1], acc);
+            acc = fmaf(h4.z, w[4 * i4 + 2], acc);
+            acc = fmaf(h4.w, w[4 * i4 + 3], acc);
+        }
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        if (writer) {
+            const float h = tanhf((p + acc) + bias);
+            hs[cur ^ 1][jq * RNN_QS + ji] = h;
+            prow[t * tstride] = h;
+        }
+        cur ^= 1;
+        __syncthreads();
+    }
+}
+
+int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
+                     float* hid, int T, int B, int H, hipStream_t s) {
+    if (H > RNN_HMAX) return ASR_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(rnn_recur_kernel, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid,
+                       T, B, H);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// z = x + lam*y (cublasSgeam with alpha = 1, beta = lam: cuMatrix.cpp:150).
+template <bool VEC4>
+__global__ __launch_bounds__(256) void axpy_kernel(const float* __restrict__ x,
+                                                   const float* __restrict__ y,
+                                                   float* __restrict__ z, long n, float lam) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (VEC4) {
+        if (i < (n >> 2)) {
+            const float4 a = reinterpret_cast<const float4*>(x)[i];
+            const float4 c = reinterpret_cast<const float4*>(y)[i];
+            reinterpret_cast<float4*>(z)[i] =
+                make_float4(a.x + lam * c.x, a.y + lam * c.y, a.z + lam * c.z, a.w + lam * c.w);
+        }
+    } else if (i < n) {
+        z[i] = x[i] + lam * y[i];
+    }
+}
+
+// h_0 = tanh(P_0 + (b_hh + b_ih)) when h_{-1} = 0 (RNN_Cell.cu:10-12 with hh = 0).
+__global__ __launch_bounds__(256) void bias_tanh_kernel(float* __restrict__ p,
+                                                        const float* __restrict__ b_ih,
+                                                        const float* __restrict__ b_hh, long n,
+                                                        int H) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const int j = (int)(i % H);
+        p[i] = tanhf(p[i] + (b_hh[j] + b_ih[j]));
+    }
+}
+
+int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s) {
+    if (n <= 0) return ASR_OK;
+    hipLaunchKernelGGL(bias_tanh_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, b_ih,
+                       b_hh, n, H);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s) {
+    if (n <= 0) return ASR_OK;
+    const bool vec = (n % 4) == 0 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)z) % 16) == 0;
+    const long work = vec ? n / 4 : n;
+    const dim3 grid((unsigned)((work + 255) / 256));
+    if (vec) hipLaunchKernelGGL(axpy_kernel<true>, grid, dim3(256), 0, s, x, y, z, n, lam);
+    else hipLaunchKernelGGL(axpy_kernel<false>, grid, dim3(256), 0, s, x, y, z, n, lam);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+}  // namespace asr

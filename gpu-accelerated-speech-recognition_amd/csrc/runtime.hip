@@ -1,0 +1,498 @@
+// ============================================================================
+// libasr_amd.so host runtime: the C ABI of include/asr_amd.h.
+// Memory (MemoryMonitor / cuMatrix transfers), dense ops (Linear / RNN_Cell /
+// RNN / matrixMul / matrixAdd) and the CTC decoder handle (CTCBeamSearch).
+// ============================================================================
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ctc_beam.h"
+#include "dense.h"
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+void asr_internal_set_error(const char* what, const char* msg, const char* file, int line) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s: %s (%s:%d)", what, msg, file, line);
+    g_last_error = buf;
+    if (getenv("ASR_VERBOSE")) fprintf(stderr, "[asr] %s\n", buf);
+}
+
+extern "C" {
+
+const char* asr_status_string(int status) {
+    switch (status) {
+        case ASR_OK: return "ok";
+        case ASR_ERR_ARG: return "invalid argument";
+        case ASR_ERR_HIP: return g_last_error.empty() ? "HIP runtime error" : g_last_error.c_str();
+        case ASR_ERR_OOM: return "out of memory";
+        case ASR_ERR_BEAM_OVERFLOW: return "beam overflow: more tied survivors than max_states";
+        case ASR_ERR_UNSUPPORTED: return "unsupported shape";
+        case ASR_ERR_STATE: return "invalid call order";
+        default: return "unknown status";
+    }
+}
+
+const char* asr_version(void) { return "libasr_amd gfx950 r1"; }
+
+// ------------------------------------------------------------- device/memory
+int asr_get_device_count(int* count) {
+    if (!count) return ASR_ERR_ARG;
+    ASR_HIP_TRY(hipGetDeviceCount(count));
+    return ASR_OK;
+}
+int asr_set_device(int device) {
+    ASR_HIP_TRY(hipSetDevice(device));
+    return ASR_OK;
+}
+int asr_get_device(int* device) {
+    if (!device) return ASR_ERR_ARG;
+    ASR_HIP_TRY(hipGetDevice(device));
+    return ASR_OK;
+}
+int asr_device_malloc(void** p, size_t bytes) {
+    if (!p) return ASR_ERR_ARG;
+    *p = nullptr;
+    if (bytes == 0) return ASR_OK;
+    ASR_HIP_TRY(hipMalloc(p, bytes));
+    ASR_HIP_TRY(hipMemset(*p, 0, bytes));   // cuMatrix.h:222 zero-fills on allocation
+    return ASR_OK;
+}
+int asr_device_free(void* p) {
+    if (p) ASR_HIP_TRY(hipFree(p));
+    return ASR_OK;
+}
+int asr_host_malloc(void** p, size_t bytes) {
+    if (!p) return ASR_ERR_ARG;
+    *p = nullptr;
+    if (bytes == 0) return ASR_OK;
+    ASR_HIP_TRY(hipHostMalloc(p, bytes, hipHostMallocPortable));
+    memset(*p, 0, bytes);
+    return ASR_OK;
+}
+int asr_host_free(void* p) {
+    if (p) ASR_HIP_TRY(hipHostFree(p));
+    return ASR_OK;
+}
+static int copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, asr_stream_t s) {
+    if (bytes == 0) return ASR_OK;
+    if (!dst || !src) return ASR_ERR_ARG;
+    ASR_HIP_TRY(hipMemcpyAsync(dst, src, bytes, kind, asr_stream(s)));
+    if (kind != hipMemcpyDeviceToDevice) ASR_HIP_TRY(hipStreamSynchronize(asr_stream(s)));
+    return ASR_OK;
+}
+int asr_memcpy_h2d(void* d, const void* h, size_t n, asr_stream_t s) { return copy(d, h, n, hipMemcpyHostToDevice, s); }
+int asr_memcpy_d2h(void* h, const void* d, size_t n, asr_stream_t s) { return copy(h, d, n, hipMemcpyDeviceToHost, s); }
+int asr_memcpy_d2d(void* d, const void* e, size_t n, asr_stream_t s) { return copy(d, e, n, hipMemcpyDeviceToDevice, s); }
+int asr_memset(void* d, int v, size_t n, asr_stream_t s) {
+    if (n == 0) return ASR_OK;
+    if (!d) return ASR_ERR_ARG;
+    ASR_HIP_TRY(hipMemsetAsync(d, v, n, asr_stream(s)));
+    return ASR_OK;
+}
+int asr_stream_create(asr_stream_t* s) {
+    if (!s) return ASR_ERR_ARG;
+    hipStream_t st;
+    ASR_HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    *s = (asr_stream_t)st;
+    return ASR_OK;
+}
+int asr_stream_destroy(asr_stream_t s) {
+    if (s) ASR_HIP_TRY(hipStreamDestroy(asr_stream(s)));
+    return ASR_OK;
+}
+int asr_stream_sync(asr_stream_t s) {
+    ASR_HIP_TRY(hipStreamSynchronize(asr_stream(s)));
+    return ASR_OK;
+}
+int asr_device_sync(void) {
+    ASR_HIP_TRY(hipDeviceSynchronize());
+    return ASR_OK;
+}
+
+// ----------------------------------------------------------------- dense ops
+static asr::GemmArgs gemm_args(const float* A, const float* B, float* C, int M, int K, int N) {
+    asr::GemmArgs g{};
+    g.A = A; g.B = B; g.C = C;
+    g.M = M; g.N = N; g.K = K;
+    g.sam = K; g.sak = 1; g.sbk = N; g.sbn = 1; g.ldc = N;
+    return g;
+}
+
+int asr_matmul(const float* x, const float* y, float* z, int M, int K, int N, asr_stream_t s) {
+    if (!x || !y || !z || M <= 0 || K <= 0 || N <= 0) return ASR_ERR_ARG;
+    return asr::gemm_launch(gemm_args(x, y, z, M, K, N), asr::EPI_NONE, asr_stream(s));
+}
+int asr_matmul_ta(const float* x, const float* y, float* z, int M, int K, int N, asr_stream_t s) {
+    // z[K,N] = x[M,K]^T . y[M,N]: GEMM rows = K, inner = M.
+    if (!x || !y || !z || M <= 0 || K <= 0 || N <= 0) return ASR_ERR_ARG;
+    asr::GemmArgs g = gemm_args(x, y, z, K, M, N);
+    g.sam = 1; g.sak = K;   // A(r, m) = x[m][r]
+    return asr::gemm_launch(g, asr::EPI_NONE, asr_stream(s));
+}
+int asr_matmul_tb(const float* x, const float* y, float* z, int M, int K, int N, asr_stream_t s) {
+    // z[M,N] = x[M,K] . y[N,K]^T
+    if (!x || !y || !z || M <= 0 || K <= 0 || N <= 0) return ASR_ERR_ARG;
+    asr::GemmArgs g = gemm_args(x, y, z, M, K, N);
+    g.sbk = 1; g.sbn = K;   // B(k, n) = y[n][k]
+    return asr::gemm_launch(g, asr::EPI_NONE, asr_stream(s));
+}
+int asr_matadd(const float* x, const float* y, float* z, int M, int N, float lambda, asr_stream_t s) {
+    if (!x || !y || !z || M <= 0 || N <= 0) return ASR_ERR_ARG;
+    return asr::axpy_launch(x, y, z, (long)M * N, lambda, asr_stream(s));
+}
+int asr_linear_fwd(const float* x, const float* W, const float* b, float* y, int M, int K, int N,
+                   int epilogue, asr_stream_t s) {
+    if (!x || !W || !y || M <= 0 || K <= 0 || N <= 0) return ASR_ERR_ARG;
+    if (epilogue != ASR_EPI_NONE && !b) return ASR_ERR_ARG;
+    asr::GemmArgs g = gemm_args(x, W, y, M, K, N);
+    g.b1 = b;
+    int epi;
+    switch (epilogue) {
+        case ASR_EPI_NONE: epi = asr::EPI_NONE; break;
+        case ASR_EPI_BIAS: epi = asr::EPI_BIAS; break;
+        case ASR_EPI_BIAS_RELU: epi = asr::EPI_BIAS_RELU; break;
+        case ASR_EPI_BIAS_LOGSOFTMAX: epi = asr::EPI_LOGSOFTMAX; break;
+        default: return ASR_ERR_ARG;
+    }
+    return asr::gemm_launch(g, epi, asr_stream(s));
+}
+int asr_rnn_cell_fwd(const float* x, const float* h_prev, const float* W_ih, const float* W_hh,
+                     const float* b_ih, const float* b_hh, float* h_out, int B, int in, int H,
+                     asr_stream_t s) {
+    if (!x || !h_prev || !W_ih || !W_hh || !b_ih || !b_hh || !h_out || B <= 0 || in <= 0 || H <= 0)
+        return ASR_ERR_ARG;
+    asr::GemmArgs g = gemm_args(x, W_ih, h_out, B, in, H);
+    g.A2 = h_prev; g.B2 = W_hh; g.K2 = H;
+    g.b1 = b_ih; g.b2 = b_hh;
+    return asr::gemm_launch(g, asr::EPI_DUAL_TANH, asr_stream(s));
+}
+int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float* W_hh,
+                const float* b_ih, const float* b_hh, float* hid, int T, int B, int in, int H,
+                asr_stream_t s) {
+    if (!x || !W_ih || !W_hh || !b_ih || !b_hh || !hid || T <= 0 || B <= 0 || in <= 0 || H <= 0)
+        return ASR_ERR_ARG;
+    if (x == hid) return ASR_ERR_ARG;
+    const hipStream_t st = asr_stream(s);
+    // 1. input projection for all T at once: hid = x . W_ih   ([T*B, in] x [in, H])
+    int rc = asr::gemm_launch(gemm_args(x, W_ih, hid, T * B, in, H), asr::EPI_NONE, st);
+    if (rc) return rc;
+    // 2. recurrence, in place over hid.
+    if (H <= 256) return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+    // H > 256: one fused cell GEMM per step, h_t = tanh((P_t + h_{t-1}.W_hh) + bias).
+    for (int t = 0; t < T; t++) {
+        float* ht = hid + (size_t)t * B * H;
+        const float* hp = t == 0 ? h0 : hid + (size_t)(t - 1) * B * H;
+        if (!hp) {   // h_{-1} = 0 (RNN.h:15-16 zero-filled h_0s)
+            rc = asr::bias_tanh_launch(ht, b_ih, b_hh, (long)B * H, H, st);
+        } else {
+            asr::GemmArgs g = gemm_args(hp, W_hh, ht, B, H, H);
+            g.D = ht; g.b1 = b_ih; g.b2 = b_hh;
+            rc = asr::gemm_launch(g, asr::EPI_ADD_TANH, st);
+        }
+        if (rc) return rc;
+    }
+    return ASR_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- CTC handle
+struct asr_ctc {
+    int V, beam, blank, K, kcap, waves_override;
+    std::vector<int32_t> codes;
+    uint64_t blank_less;
+    int device;
+    // workspace (device)
+    int capB = 0, capT = 0;
+    int2* d_nodes = nullptr;
+    int *d_fin_n = nullptr, *d_fin_node = nullptr, *d_status = nullptr;
+    double* d_fin_score = nullptr;
+    int *d_best_lab = nullptr, *d_best_len = nullptr;
+    double* d_best_score = nullptr;
+    int* d_codes = nullptr;
+    int *d_all_lab = nullptr, *d_all_len = nullptr;
+    size_t cap_all = 0;
+    // pinned host mirrors of the best-path results
+    int *h_best_lab = nullptr, *h_best_len = nullptr, *h_status = nullptr;
+    double* h_best_score = nullptr;
+    // last decode
+    bool have = false;
+    int lastT = 0, lastB = 0, last_waves = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    asr::CtcArgs args{};
+};
+
+namespace {
+
+int auto_waves(int K) { return K <= 64 ? 1 : (K <= 160 ? 2 : 4); }
+
+asr::CtcGeom plan(const asr_ctc* h, int waves) {
+    asr::CtcGeom g{};
+    g.V = h->V;
+    g.blank = h->blank;
+    g.K = h->K;
+    g.kcap = h->kcap;
+    g.sb = (h->V + 1) <= 32 ? 5 : 6;
+    const int nt = 64 * waves;
+    g.ch = std::max(1, std::min(32, 16 * nt / h->V));
+    int ht = 64;
+    while (ht < 2 * h->kcap) ht <<= 1;
+    g.ht = ht;
+    return g;
+}
+
+void free_ws(asr_ctc* h) {
+    hipFree(h->d_nodes); hipFree(h->d_fin_n); hipFree(h->d_fin_node); hipFree(h->d_status);
+    hipFree(h->d_fin_score); hipFree(h->d_best_lab); hipFree(h->d_best_len);
+    hipFree(h->d_best_score);
+    hipHostFree(h->h_best_lab); hipHostFree(h->h_best_len); hipHostFree(h->h_status);
+    hipHostFree(h->h_best_score);
+    h->d_nodes = nullptr; h->d_fin_n = h->d_fin_node = h->d_status = nullptr;
+    h->d_fin_score = nullptr; h->d_best_lab = h->d_best_len = nullptr; h->d_best_score = nullptr;
+    h->h_best_lab = h->h_best_len = h->h_status = nullptr; h->h_best_score = nullptr;
+    h->capB = h->capT = 0;
+}
+
+int ensure_ws(asr_ctc* h, int B, int T) {
+    if (B <= h->capB && T <= h->capT) return ASR_OK;
+    // Grow geometrically in B and T so that repeated decodes do not thrash.
+    const int nB = std::max(B, h->capB), nT = std::max(T, h->capT);
+    hipDeviceSynchronize();
+    free_ws(h);
+    const size_t kc = (size_t)h->kcap;
+    ASR_HIP_TRY(hipMalloc(&h->d_nodes, sizeof(int2) * (size_t)nB * nT * kc));
+    ASR_HIP_TRY(hipMalloc(&h->d_fin_n, sizeof(int) * nB));
+    ASR_HIP_TRY(hipMalloc(&h->d_status, sizeof(int) * nB));
+    ASR_HIP_TRY(hipMalloc(&h->d_fin_node, sizeof(int) * nB * kc));
+    ASR_HIP_TRY(hipMalloc(&h->d_fin_score, sizeof(double) * nB * kc));
+    ASR_HIP_TRY(hipMalloc(&h->d_best_lab, sizeof(int) * (size_t)nB * nT));
+    ASR_HIP_TRY(hipMalloc(&h->d_best_len, sizeof(int) * nB));
+    ASR_HIP_TRY(hipMalloc(&h->d_best_score, sizeof(double) * nB));
+    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_best_lab, sizeof(int) * (size_t)nB * nT, 0));
+    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_best_len, sizeof(int) * nB, 0));
+    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_status, sizeof(int) * nB, 0));
+    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_best_score, sizeof(double) * nB, 0));
+    h->capB = nB;
+    h->capT = nT;
+    return ASR_OK;
+}
+
+// String order of two label sequences under the symbol codes.
+bool code_less(const asr_ctc* h, const int* a, int la, const int* b, int lb) {
+    const int n = std::min(la, lb);
+    for (int i = 0; i < n; i++) {
+        const int ca = h->codes[a[i]], cb = h->codes[b[i]];
+        if (ca != cb) return ca < cb;
+    }
+    return la < lb;
+}
+
+}  // namespace
+
+extern "C" {
+
+int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, int max_states,
+                   asr_ctc_t** out) {
+    if (!out) return ASR_ERR_ARG;
+    *out = nullptr;
+    if (V < 2 || beam_width < 1 || blank_id < 0 || blank_id >= V) return ASR_ERR_ARG;
+    if (V > 63) return ASR_ERR_UNSUPPORTED;
+    asr_ctc* h = new asr_ctc();
+    h->V = V;
+    h->beam = beam_width;
+    h->blank = blank_id;
+    h->K = beam_width + 1;
+    h->codes.resize(V);
+    for (int v = 0; v < V; v++) h->codes[v] = codes ? codes[v] : v;
+    for (int v = 0; v < V; v++)
+        for (int u = 0; u < v; u++)
+            if (h->codes[u] == h->codes[v]) { delete h; return ASR_ERR_ARG; }
+    h->blank_less = 0;
+    for (int v = 0; v < V; v++)
+        if (h->codes[blank_id] < h->codes[v]) h->blank_less |= 1ull << v;
+    int kcap = max_states > 0 ? max_states : h->K + std::max(16, h->K / 4);
+    if (kcap < h->K) { delete h; return ASR_ERR_ARG; }
+    kcap = (kcap + 31) & ~31;
+    h->kcap = kcap;
+    h->waves_override = 0;
+    if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
+    if (asr::ctc_lds_bytes(plan(h, 4)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
+    int rc = asr::ctc_set_max_lds();
+    if (rc) { delete h; return rc; }
+    if (hipGetDevice(&h->device) != hipSuccess ||
+        hipMalloc(&h->d_codes, sizeof(int) * V) != hipSuccess ||
+        hipMemcpy(h->d_codes, h->codes.data(), sizeof(int) * V, hipMemcpyHostToDevice) != hipSuccess ||
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        delete h;
+        return ASR_ERR_HIP;
+    }
+    *out = h;
+    return ASR_OK;
+}
+
+int asr_ctc_destroy(asr_ctc_t* h) {
+    if (!h) return ASR_OK;
+    hipDeviceSynchronize();
+    free_ws(h);
+    hipFree(h->d_codes);
+    hipFree(h->d_all_lab);
+    hipFree(h->d_all_len);
+    if (h->ev0) hipEventDestroy(h->ev0);
+    if (h->ev1) hipEventDestroy(h->ev1);
+    delete h;
+    return ASR_OK;
+}
+
+int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
+    if (!h || !(waves == 0 || waves == 1 || waves == 2 || waves == 4)) return ASR_ERR_ARG;
+    h->waves_override = waves;
+    return ASR_OK;
+}
+
+int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes) {
+    if (!h) return ASR_ERR_ARG;
+    const int w = h->waves_override ? h->waves_override : auto_waves(h->K);
+    if (max_states) *max_states = h->kcap;
+    if (waves) *waves = w;
+    if (lds_bytes) *lds_bytes = (int)asr::ctc_lds_bytes(plan(h, w));
+    return ASR_OK;
+}
+
+int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, asr_stream_t s) {
+    if (!h || !d_emis || T < 1 || B < 1) return ASR_ERR_ARG;
+    int rc = ensure_ws(h, B, T);
+    if (rc) return rc;
+    const int waves = h->waves_override ? h->waves_override : auto_waves(h->K);
+    asr::CtcArgs& a = h->args;
+    a.g = plan(h, waves);
+    a.emis = d_emis;
+    a.T = T;
+    a.B = B;
+    a.is_log = is_log ? 1 : 0;
+    a.blank_less = h->blank_less;
+    a.nodes = h->d_nodes;
+    a.fin_n = h->d_fin_n;
+    a.fin_node = h->d_fin_node;
+    a.fin_score = h->d_fin_score;
+    a.status = h->d_status;
+    a.best_lab = h->d_best_lab;
+    a.best_len = h->d_best_len;
+    a.best_score = h->d_best_score;
+    const hipStream_t st = asr_stream(s);
+    ASR_HIP_TRY(hipEventRecord(h->ev0, st));
+    rc = asr::ctc_launch_decode(a, waves, st);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(h->ev1, st));
+    rc = asr::ctc_launch_best(a, h->d_codes, st);
+    if (rc) return rc;
+    h->have = true;
+    h->lastT = T;
+    h->lastB = B;
+    h->last_waves = waves;
+    h->stream = st;
+    return ASR_OK;
+}
+
+int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* lengths, double* logp) {
+    if (!h || (!labels && max_len > 0)) return ASR_ERR_ARG;
+    if (!h->have) return ASR_ERR_STATE;
+    const int B = h->lastB, T = h->lastT;
+    const hipStream_t st = h->stream;
+    ASR_HIP_TRY(hipMemcpyAsync(h->h_best_len, h->d_best_len, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipMemcpyAsync(h->h_best_score, h->d_best_score, sizeof(double) * B, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipMemcpyAsync(h->h_status, h->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    const int ncol = std::min(T, std::max(max_len, 1));
+    ASR_HIP_TRY(hipMemcpy2DAsync(h->h_best_lab, sizeof(int) * ncol, h->d_best_lab, sizeof(int) * T,
+                                 sizeof(int) * ncol, B, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipStreamSynchronize(st));
+    int overflow = 0;
+    for (int b = 0; b < B; b++) {
+        const int len = h->h_best_len[b];
+        if (lengths) lengths[b] = len;
+        if (logp) logp[b] = h->h_best_score[b];
+        overflow |= h->h_status[b];
+        if (labels) {
+            const int* fwd = h->h_best_lab + (size_t)b * ncol;
+            const int n = std::min(len, max_len);
+            for (int i = 0; i < n; i++) labels[(size_t)b * max_len + i] = fwd[i];
+        }
+    }
+    return overflow ? ASR_ERR_BEAM_OVERFLOW : ASR_OK;
+}
+
+int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, int32_t* lengths,
+                      int32_t* labels, double* logp) {
+    if (!h || max_hyps < 1 || max_len < 0) return ASR_ERR_ARG;
+    if (!h->have) return ASR_ERR_STATE;
+    const int B = h->lastB, T = h->lastT, kc = h->kcap;
+    const hipStream_t st = h->stream;
+    const size_t need = (size_t)B * kc * T;
+    if (need > h->cap_all) {
+        hipStreamSynchronize(st);
+        hipFree(h->d_all_lab);
+        hipFree(h->d_all_len);
+        h->d_all_lab = nullptr; h->d_all_len = nullptr; h->cap_all = 0;
+        ASR_HIP_TRY(hipMalloc(&h->d_all_lab, sizeof(int) * need));
+        ASR_HIP_TRY(hipMalloc(&h->d_all_len, sizeof(int) * (size_t)B * kc));
+        h->cap_all = need;
+    }
+    int rc = asr::ctc_launch_all(h->args, h->d_all_lab, h->d_all_len, st);
+    if (rc) return rc;
+    std::vector<int> fin_n(B), all_len((size_t)B * kc), status(B);
+    std::vector<double> score((size_t)B * kc);
+    std::vector<int> lab(need);
+    ASR_HIP_TRY(hipMemcpyAsync(fin_n.data(), h->d_fin_n, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipMemcpyAsync(status.data(), h->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipMemcpyAsync(score.data(), h->d_fin_score, sizeof(double) * B * kc, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipMemcpyAsync(all_len.data(), h->d_all_len, sizeof(int) * B * kc, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipMemcpyAsync(lab.data(), h->d_all_lab, sizeof(int) * need, hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipStreamSynchronize(st));
+    int overflow = 0;
+    std::vector<std::vector<int>> fwd;
+    for (int b = 0; b < B; b++) {
+        overflow |= status[b];
+        const int n = fin_n[b];
+        fwd.assign(n, {});
+        std::vector<int> order(n);
+        for (int i = 0; i < n; i++) {
+            const int len = all_len[(size_t)b * kc + i];
+            const int* src = lab.data() + ((size_t)b * kc + i) * T;
+            fwd[i].assign(src, src + len);
+            order[i] = i;
+        }
+        const double* sc = score.data() + (size_t)b * kc;
+        std::sort(order.begin(), order.end(), [&](int x, int y) {
+            if (sc[x] != sc[y]) return sc[x] > sc[y];
+            return code_less(h, fwd[x].data(), (int)fwd[x].size(), fwd[y].data(), (int)fwd[y].size());
+        });
+        if (n_hyps) n_hyps[b] = n;
+        for (int k = 0; k < std::min(n, max_hyps); k++) {
+            const int i = order[k];
+            const size_t base = (size_t)b * max_hyps + k;
+            if (lengths) lengths[base] = (int)fwd[i].size();
+            if (logp) logp[base] = sc[i];
+            if (labels)
+                for (int x = 0; x < (int)fwd[i].size() && x < max_len; x++)
+                    labels[base * max_len + x] = fwd[i][x];
+        }
+    }
+    return overflow ? ASR_ERR_BEAM_OVERFLOW : ASR_OK;
+}
+
+int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms) {
+    if (!h || !ms) return ASR_ERR_ARG;
+    if (!h->have) return ASR_ERR_STATE;
+    ASR_HIP_TRY(hipEventSynchronize(h->ev1));
+    ASR_HIP_TRY(hipEventElapsedTime(ms, h->ev0, h->ev1));
+    return ASR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,160 @@
+/*
+ * asr_amd.h — C ABI of libasr_amd.so, the MI355X (gfx950) RNN + CTC
+ * beam-search decode path.
+ *
+ * This is the drop-in boundary.  The reference (jrxk/GPU-Accelerated-Speech-
+ * Recognition, mounted at /root/reference) is C++/CUDA with no FFI of its own;
+ * its callers (main.cpp, nn_test.cpp) use the C++ classes cuMatrix / Linear /
+ * RNN / RNN_Cell / CTCBeamSearch.  Those classes are re-implemented in
+ * gpu-accelerated-speech-recognition_amd/api/ on top of THIS interface, and
+ * every entry point below names the reference member it replaces.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Pointers named d_* are device pointers
+ *    (from asr_device_malloc or any other HIP allocation on the current
+ *    device); h_* are host pointers.
+ *  - Matrices are row-major fp32, exactly as cuMatrix stores them
+ *    (cuMatrix.h:12 "rows-major"); weights are [in][out] (Linear.cu:13,
+ *    RNN_Cell.cu:16-17).
+ *  - Emissions are time-major [T][B][V] (CTCBeamSearch.cu:67-69
+ *    getBatchAtT; RNN.cu:20 writes hiddens at offset t*B*H).
+ *  - asr_stream_t is a hipStream_t; NULL means the default stream.
+ *  - Every call returns an asr_status (0 = ASR_OK).  No exception crosses
+ *    this boundary.  The reference prints and calls exit(0) instead
+ *    (cuMatrix.h:85,103,207,218; cuMatrix.cpp:35-41; CTCBeamSearch.cu:267-270);
+ *    the C++ layer in api/ restores that behaviour for drop-in callers.
+ *  - All calls are asynchronous on the given stream unless documented.
+ */
+#ifndef ASR_AMD_H_
+#define ASR_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* asr_stream_t;
+
+typedef enum asr_status {
+    ASR_OK = 0,
+    ASR_ERR_ARG = 1,            /* bad argument / shape mismatch           */
+    ASR_ERR_HIP = 2,            /* HIP runtime error                       */
+    ASR_ERR_OOM = 3,            /* device or pinned host allocation failed */
+    ASR_ERR_BEAM_OVERFLOW = 4,  /* more tied survivors than max_states     */
+    ASR_ERR_UNSUPPORTED = 5,    /* shape outside what the kernels support  */
+    ASR_ERR_STATE = 6           /* call out of order (e.g. no decode yet)  */
+} asr_status;
+
+const char* asr_status_string(int status);
+/* Library build identification ("gfx950 ..."). */
+const char* asr_version(void);
+
+/* ---- device / memory: replaces MemoryMonitor (MemoryMonitor.cpp:9-51) and
+ *      the cudaMemcpy/cudaMemset calls of cuMatrix (cuMatrix.h:72-130). ---- */
+int asr_get_device_count(int* count);
+int asr_set_device(int device);
+int asr_get_device(int* device);
+int asr_device_malloc(void** d_ptr, size_t bytes);     /* MemoryMonitor::gpuMalloc, zero-filled */
+int asr_device_free(void* d_ptr);                      /* MemoryMonitor::freeGpuMemory */
+int asr_host_malloc(void** h_ptr, size_t bytes);       /* MemoryMonitor::cpuMalloc (pinned) */
+int asr_host_free(void* h_ptr);                        /* MemoryMonitor::freeCpuMemory */
+int asr_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes, asr_stream_t s); /* cuMatrix::toGpu */
+int asr_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes, asr_stream_t s); /* cuMatrix::toCpu */
+int asr_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes, asr_stream_t s);
+int asr_memset(void* d_ptr, int value, size_t bytes, asr_stream_t s);             /* cuMatrix::gpuClear */
+int asr_stream_create(asr_stream_t* s);
+int asr_stream_destroy(asr_stream_t s);
+int asr_stream_sync(asr_stream_t s);
+int asr_device_sync(void);
+
+/* ---- dense ops (MFMA fp32) ---------------------------------------------- */
+
+/* z[M,N] = x[M,K] . y[K,N]  — cuMatrix.cpp:33-70 matrixMul (cublasSgemm). */
+int asr_matmul(const float* d_x, const float* d_y, float* d_z, int M, int K, int N,
+               asr_stream_t s);
+/* matrixMulTA (cuMatrix.cpp:73-107): z[K,N] = x[M,K]^T . y[M,N] */
+int asr_matmul_ta(const float* d_x, const float* d_y, float* d_z, int M, int K, int N,
+                  asr_stream_t s);
+/* matrixMulTB (cuMatrix.cpp:110-145): z[M,N] = x[M,K] . y[N,K]^T */
+int asr_matmul_tb(const float* d_x, const float* d_y, float* d_z, int M, int K, int N,
+                  asr_stream_t s);
+/* z = x + lambda*y over M*N elements — cuMatrix.cpp:147-168 matrixAdd (cublasSgeam). */
+int asr_matadd(const float* d_x, const float* d_y, float* d_z, int M, int N, float lambda,
+               asr_stream_t s);
+
+typedef enum asr_epilogue {
+    ASR_EPI_NONE = 0,            /* y = x.W                                         */
+    ASR_EPI_BIAS = 1,            /* y = x.W + b                                     */
+    ASR_EPI_BIAS_RELU = 2,       /* y = max(x.W + b, 0)  — Linear.cu:3-10 ReLU      */
+    ASR_EPI_BIAS_LOGSOFTMAX = 3  /* y = log_softmax(x.W + b) per row (model.py:49)  */
+} asr_epilogue;
+
+/* Linear::forward (Linear.cu:42-49): y[M,N] = epi(x[M,K] . W[K,N] + b[N]).
+ * ASR_EPI_BIAS_LOGSOFTMAX needs N <= 64. */
+int asr_linear_fwd(const float* d_x, const float* d_W, const float* d_b, float* d_y, int M,
+                   int K, int N, int epilogue, asr_stream_t s);
+
+/* RNN_Cell::forward (RNN_Cell.cu:65-74):
+ * h_out[B,H] = tanh((x[B,in].W_ih[in,H] + h_prev[B,H].W_hh[H,H]) + (b_hh + b_ih)). */
+int asr_rnn_cell_fwd(const float* d_x, const float* d_h_prev, const float* d_W_ih,
+                     const float* d_W_hh, const float* d_b_ih, const float* d_b_hh,
+                     float* d_h_out, int B, int in, int H, asr_stream_t s);
+
+/* One RNN layer over a whole sequence — RNN::forward (RNN.cu:9-30) for one
+ * layer: x time-major [T*B, in], h0 [B,H] (NULL = zeros, RNN.h:15-16),
+ * hiddens [T*B, H].  The input projection for all T is one MFMA GEMM; the
+ * recurrence runs in one launch with W_hh resident on chip (H <= 256) or as
+ * T fused cell launches otherwise. */
+int asr_rnn_fwd(const float* d_x, const float* d_h0, const float* d_W_ih, const float* d_W_hh,
+                const float* d_b_ih, const float* d_b_hh, float* d_hiddens, int T, int B,
+                int in, int H, asr_stream_t s);
+
+/* ---- CTC prefix beam search: replaces CTCBeamSearch (CTCBeamSearch.h:107-150,
+ *      CTCBeamSearch.cu:220-312) with the semantics of the CPU decoder
+ *      CTCBeamSearch.cpp:50-187 (fixes F1-F3, fp64 log domain). ---- */
+typedef struct asr_ctc asr_ctc_t;
+
+/* Constructor CTCBeamSearch(char* vocab, int vocabSize, int beamWidth, int blankID)
+ * (h:107).  codes[V] is the symbol code of each label (the vocab char as
+ * unsigned char for the reference API; NULL = label id).  Hypothesis order on
+ * ties is code-string order, as std::string order in the reference.
+ * max_states bounds the beam incl. ties at the cutoff (0 = automatic,
+ * >= beamWidth+1). */
+int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, int max_states,
+                   asr_ctc_t** out);
+int asr_ctc_destroy(asr_ctc_t* h);
+
+/* CTCBeamSearch::decode(seqProb, timestep, batchSize) (cu:262): decode B
+ * utterances of d_emis[T][B][V] (probabilities, or log-probabilities if
+ * is_log).  Enqueues the decode and the best-path traceback on stream s; the
+ * workspace is sized once and reused (the reference re-allocated per call,
+ * cu:263).  Fetch results with asr_ctc_get_best / asr_ctc_get_beams. */
+int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, asr_stream_t s);
+
+/* Best hypothesis of each utterance (cpp:74-84: max score, first in string
+ * order on ties).  Synchronises the decode stream.  h_labels[B][max_len]
+ * (label ids), h_lengths[B], h_logp[B] (fp64 log-probability).
+ * Returns ASR_ERR_BEAM_OVERFLOW if an utterance had more tied survivors than
+ * max_states (its result is then not the reference's). */
+int asr_ctc_get_best(asr_ctc_t* h, int32_t* h_labels, int max_len, int32_t* h_lengths,
+                     double* h_logp);
+
+/* Full final beam of every utterance, ranked by (logp desc, string asc):
+ * h_n_hyps[B], h_lengths[B][max_hyps], h_labels[B][max_hyps][max_len],
+ * h_logp[B][max_hyps].  Runs a traceback over all final hypotheses. */
+int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps,
+                      int32_t* h_lengths, int32_t* h_labels, double* h_logp);
+
+/* Device time of the last decode's beam-search kernel (ms, HIP events on the
+ * decode stream) and its launch geometry; for roofline accounting. */
+int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms);
+/* Tuning knobs: waves per utterance (1, 2 or 4; 0 = automatic). */
+int asr_ctc_set_waves(asr_ctc_t* h, int waves);
+int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASR_AMD_H_ */

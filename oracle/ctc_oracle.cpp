@@ -1,0 +1,295 @@
+// ============================================================================
+// TEST INFRASTRUCTURE ONLY — parity oracle for the CTC beam-search decoder.
+//
+// This file is a CPU restatement of the reference CPU decoder
+// /root/reference/CTCBeamSearch.cpp (jrxk/GPU-Accelerated-Speech-Recognition).
+// It is linked only by tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg, as the checker. The product path (libasr_amd.so) never
+// links, loads or calls it.
+//
+// Parity status: the reference decoder itself is unbuildable in this image
+// (CTCBeamSearch.cpp does not compile against its own CTCBeamSearch.h and
+// needs cublas_v2.h / helper_cuda.h, which the image lacks — see DESIGN.md).
+// This restatement is pinned instead by
+//   (1) exhaustive CTC enumeration on small cases (no pruning => exact
+//       prefix probabilities; tests/test_oracle.py),
+//   (2) the reference's only decoder test vector, main.cpp:51-60, whose
+//       result under the fixed semantics is recorded in SURVEY.md A.6,
+//   (3) a literal prob-domain fp32 variant of the same code
+//       (oracle_ctc_decode_prob) that the log-domain one must agree with.
+//
+// Structure follows the reference one-to-one: std::set of state strings,
+// std::map of scores, the same loop order (cpp:64-70), the same transition
+// rule (cpp:128-157), the same prune (cpp:97-118) and final merge
+// (cpp:169-187), with the three minimal fixes of SURVEY.md Appendix A.1:
+//   F1 prune visits every state exactly once (cpp:110-117 advanced twice),
+//   F2 prune keeps everything when #states <= beamWidth (cpp:107 threw),
+//   F3 final merge reads pathScore[*iter], not pathScore[p] (cpp:181,184),
+// and log-domain fp64 scores (the fp32 products of cpp:134-155 underflow
+// after ~40 frames); '+=' of cpp:160 becomes log-sum-exp.
+//
+// A "state string" is a sequence of symbol codes (char16_t).  For the
+// reference's char vocab the code of label i is (unsigned char)vocab[i], so
+// std::u16string ordering equals std::string ordering (char_traits<char>
+// compares as unsigned char).
+// ============================================================================
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+typedef std::u16string Str;
+
+// lse(a, b) = log(exp(a) + exp(b)); the log-domain form of `+=` (cpp:160)
+// and of the final merge sum (cpp:181).
+inline double lse(double a, double b) {
+    if (a == -INFINITY) return b;
+    if (b == -INFINITY) return a;
+    double m = a > b ? a : b;
+    return m + std::log1p(std::exp(-std::fabs(a - b)));
+}
+
+// Score policies.  LogDomain is the parity oracle (fp64 log-probabilities).
+// ProbDomain is the reference's literal arithmetic (fp32 probability
+// products, cpp:134-155, and fp32 `+=`, cpp:160/181), used only to cross-check
+// the log-domain restatement on short utterances where fp32 does not
+// underflow.
+struct LogDomain {
+    typedef double S;
+    static S emit(double x, bool is_log) { return is_log ? x : std::log(x); }
+    static S extend(S parent, S e) { return parent + e; }
+    static S merge(S acc, S x) { return lse(acc, x); }
+};
+struct ProbDomain {
+    typedef float S;
+    static S emit(double x, bool is_log) { return is_log ? (float)std::exp(x) : (float)x; }
+    static S extend(S parent, S e) { return parent * e; }
+    static S merge(S acc, S x) { return acc + x; }
+};
+
+template <class P>
+struct OracleCTC {
+    typedef typename P::S S;
+    std::vector<char16_t> code;   // vocab[i] (h:43) as a symbol code
+    int vocabSize, beamWidth, blankID;
+    std::set<Str> path, updatePath, finalPath;                           // h:48-55
+    std::map<Str, S> pathScore, updatePathScore, finalPathScore;
+
+    OracleCTC(const std::vector<char16_t>& c, int beam, int blank)
+        : code(c), vocabSize((int)c.size()), beamWidth(beam), blankID(blank) {}
+
+    // initialPath (cpp:87-95): one state per symbol, then prune.
+    void initialPath(const S* le) {
+        for (int i = 0; i < vocabSize; i++) {
+            Str s(1, code[i]);
+            path.insert(s);
+            pathScore.insert(std::make_pair(s, le[i]));
+        }
+        prune();
+    }
+
+    // prune (cpp:97-118) with F1/F2: keep states scoring >= the
+    // (beamWidth+1)-th largest score.
+    void prune() {
+        std::vector<S> scores;
+        for (const Str& s : path) scores.push_back(pathScore.at(s));
+        std::sort(scores.begin(), scores.end(), std::greater<S>());
+        if ((int)scores.size() <= beamWidth) return;                    // F2
+        S cutoff = scores[beamWidth];
+        for (auto it = path.begin(); it != path.end();) {               // F1
+            if (pathScore.at(*it) < cutoff) {
+                pathScore.erase(*it);
+                it = path.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+
+    // extend (cpp:120-167): every state x every symbol, merged by string.
+    void extend(const S* le) {
+        updatePathScore.clear();
+        updatePath.clear();
+        const char16_t blankCh = code[blankID];
+        for (const Str& s : path) {
+            const S sc = pathScore.at(s);
+            for (int i = 0; i < vocabSize; i++) {
+                Str newPath;
+                if (i == blankID) {
+                    if (s.back() == blankCh) newPath = s;          // cpp:132-134
+                    else newPath = s + blankCh;                    // cpp:136-138
+                } else if (s.back() == blankCh) {                  // cpp:143-146
+                    newPath = s;
+                    newPath.back() = code[i];
+                } else if (s.back() == code[i]) {                  // cpp:149-150
+                    newPath = s;
+                } else {                                           // cpp:151-152
+                    newPath = s + code[i];
+                }
+                const S score = P::extend(sc, le[i]);
+                auto f = updatePathScore.find(newPath);            // cpp:159-164
+                if (f != updatePathScore.end()) {
+                    f->second = P::merge(f->second, score);
+                } else {
+                    updatePath.insert(newPath);
+                    updatePathScore[newPath] = score;
+                }
+            }
+        }
+    }
+
+    // mergeIdenticalPaths (cpp:169-187) with F3: strip the trailing blank and
+    // sum "p" with "p$" in set order.
+    void mergeIdenticalPaths() {
+        const char16_t blankCh = code[blankID];
+        for (const Str& s : path) {
+            Str p = s;
+            if (p.back() == blankCh) p.pop_back();
+            auto f = finalPathScore.find(p);
+            if (f != finalPathScore.end()) {
+                f->second = P::merge(f->second, pathScore[s]);        // F3
+            } else {
+                finalPath.insert(p);
+                finalPathScore[p] = pathScore[s];
+            }
+        }
+    }
+
+    // decode (cpp:50-85) for one utterance: le[t*V + v] emission scores.
+    void decode(const std::vector<S>& le, int T) {
+        path.clear(); pathScore.clear();
+        finalPath.clear(); finalPathScore.clear();
+        initialPath(&le[0]);
+        for (int t = 1; t < T; t++) {
+            extend(&le[(size_t)t * vocabSize]);
+            path = updatePath;                                     // cpp:67-68
+            pathScore = updatePathScore;
+            prune();                                               // cpp:69
+        }
+        mergeIdenticalPaths();                                     // cpp:72
+    }
+};
+
+struct Hyp {
+    Str s;
+    double score;
+};
+
+// Final hypotheses ranked by (score desc, string asc).  Rank 0 is exactly
+// std::max_element over finalPathScore (cpp:76-84): the first maximum in
+// std::map (string) order.
+template <class P>
+std::vector<Hyp> ranked(const OracleCTC<P>& d) {
+    std::vector<Hyp> h;
+    for (const auto& kv : d.finalPathScore) h.push_back({kv.first, (double)kv.second});
+    std::stable_sort(h.begin(), h.end(), [](const Hyp& a, const Hyp& b) {
+        return a.score > b.score;   // stable: ties keep map (string) order
+    });
+    return h;
+}
+
+}  // namespace
+
+namespace {
+
+template <class P>
+int decode_all(const float* emis, int T, int B, int V, int beam, int blank,
+               const int32_t* codes, int is_log, int nthreads, int max_hyps, int max_len,
+               int32_t* n_hyps, int32_t* lengths, int32_t* labels, double* logp) {
+    if (!emis || T < 1 || B < 1 || V < 2 || beam < 1 || blank < 0 || blank >= V ||
+        max_hyps < 1 || max_len < 1)
+        return -1;
+    std::vector<char16_t> code(V);
+    std::map<char16_t, int> label_of;
+    for (int v = 0; v < V; v++) {
+        code[v] = (char16_t)(codes ? codes[v] : v);
+        if (label_of.count(code[v])) return -1;   // codes must be distinct
+        label_of[code[v]] = v;
+    }
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > B) nthreads = B;
+    auto work = [&](int b0, int b1) {
+        OracleCTC<P> dec(code, beam, blank);
+        std::vector<typename P::S> le((size_t)T * V);
+        for (int b = b0; b < b1; b++) {
+            for (int t = 0; t < T; t++)
+                for (int v = 0; v < V; v++)
+                    le[(size_t)t * V + v] =
+                        P::emit((double)emis[((size_t)t * B + b) * V + v], is_log != 0);
+            dec.decode(le, T);
+            std::vector<Hyp> h = ranked(dec);
+            int n = (int)std::min<size_t>(h.size(), (size_t)max_hyps);
+            n_hyps[b] = (int32_t)h.size();
+            for (int k = 0; k < n; k++) {
+                size_t base = (size_t)b * max_hyps + k;
+                lengths[base] = (int32_t)h[k].s.size();
+                logp[base] = h[k].score;
+                for (int i = 0; i < (int)h[k].s.size() && i < max_len; i++)
+                    labels[base * max_len + i] = label_of[h[k].s[i]];
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int k = 0; k < nthreads; k++) {
+        int b0 = (int)((long long)B * k / nthreads), b1 = (int)((long long)B * (k + 1) / nthreads);
+        th.emplace_back(work, b0, b1);
+    }
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Decode B utterances of time-major emissions emis[T][B][V] (fp32
+// probabilities, or log-probabilities when is_log != 0) with fp64
+// log-domain scores.  codes[V] gives the symbol code of each label (NULL:
+// code = label id); string order is code order.  Utterances are split
+// statically over nthreads std::threads.  Outputs the final ranked beam of
+// every utterance, truncated to max_hyps hypotheses of at most max_len
+// labels (label ids, not codes):
+//   n_hyps[B], lengths[B][max_hyps], labels[B][max_hyps][max_len],
+//   logp[B][max_hyps]   (log-probabilities).
+// Returns 0, or -1 on bad arguments.
+int oracle_ctc_decode(const float* emis, int T, int B, int V, int beam, int blank,
+                      const int32_t* codes, int is_log, int nthreads, int max_hyps,
+                      int max_len, int32_t* n_hyps, int32_t* lengths, int32_t* labels,
+                      double* logp) {
+    return decode_all<LogDomain>(emis, T, B, V, beam, blank, codes, is_log, nthreads,
+                                 max_hyps, max_len, n_hyps, lengths, labels, logp);
+}
+
+// The reference's literal arithmetic (fp32 probability products and sums)
+// with fixes F1-F3; logp[] then holds probabilities, not logs.
+int oracle_ctc_decode_prob(const float* emis, int T, int B, int V, int beam, int blank,
+                           const int32_t* codes, int is_log, int nthreads, int max_hyps,
+                           int max_len, int32_t* n_hyps, int32_t* lengths, int32_t* labels,
+                           double* prob) {
+    return decode_all<ProbDomain>(emis, T, B, V, beam, blank, codes, is_log, nthreads,
+                                  max_hyps, max_len, n_hyps, lengths, labels, prob);
+}
+
+// Same decode, outputs discarded; returns wall seconds (cpu_baseline leg).
+double oracle_ctc_time(const float* emis, int T, int B, int V, int beam, int blank,
+                       int is_log, int nthreads) {
+    std::vector<int32_t> nh(B), len(B), lab((size_t)B * T);
+    std::vector<double> lp(B);
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = oracle_ctc_decode(emis, T, B, V, beam, blank, nullptr, is_log, nthreads, 1, T,
+                               nh.data(), len.data(), lab.data(), lp.data());
+    auto t1 = std::chrono::steady_clock::now();
+    if (rc) return -1.0;
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"

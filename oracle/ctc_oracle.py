@@ -1,0 +1,98 @@
+"""TEST INFRASTRUCTURE ONLY — Python handle on the CPU parity oracle.
+
+Loads oracle/libctc_oracle.so (built from oracle/ctc_oracle.cpp, a CPU
+restatement of /root/reference/CTCBeamSearch.cpp; see its header for the
+fixes and how it is pinned).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg use this module, and only as the checker.
+
+Also holds the synthetic emission generator used by tests and bench (the
+same inputs go to the GPU and to the oracle).
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "libctc_oracle.so"
+SEED0 = 20261015
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = ctypes.CDLL(str(LIB_PATH))
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        for name in ("oracle_ctc_decode", "oracle_ctc_decode_prob"):
+            fn = getattr(L, name)
+            fn.argtypes = [vp, i, i, i, i, i, vp, i, i, i, i, vp, vp, vp, vp]
+            fn.restype = i
+        L.oracle_ctc_time.argtypes = [vp, i, i, i, i, i, i, i]
+        L.oracle_ctc_time.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+Beam = List[Tuple[List[int], float]]
+
+
+def decode(emis: np.ndarray, beam: int, blank: int = 0, codes: Optional[Sequence[int]] = None,
+           is_log: bool = False, nthreads: int = 1, max_hyps: int = 512,
+           prob_domain: bool = False) -> List[Beam]:
+    """Ranked final beam [(labels, logp)] per utterance of emis [T][B][V]."""
+    emis = np.ascontiguousarray(emis, dtype=np.float32)
+    T, B, V = emis.shape
+    c = None if codes is None else np.ascontiguousarray(codes, dtype=np.int32)
+    nh = np.zeros(B, np.int32)
+    ln = np.zeros((B, max_hyps), np.int32)
+    lab = np.zeros((B, max_hyps, T), np.int32)
+    lp = np.zeros((B, max_hyps), np.float64)
+    fn = lib().oracle_ctc_decode_prob if prob_domain else lib().oracle_ctc_decode
+    rc = fn(emis.ctypes.data, T, B, V, beam, blank, c.ctypes.data if c is not None else None,
+            int(is_log), nthreads, max_hyps, T, nh.ctypes.data, ln.ctypes.data, lab.ctypes.data,
+            lp.ctypes.data)
+    if rc != 0:
+        raise ValueError("oracle_ctc_decode: bad arguments")
+    return [[(list(lab[b, k, :ln[b, k]]), float(lp[b, k])) for k in range(min(nh[b], max_hyps))]
+            for b in range(B)]
+
+
+def time_decode(emis: np.ndarray, beam: int, blank: int = 0, is_log: bool = False,
+                nthreads: int = 1) -> float:
+    """Wall seconds of the oracle decode (cpu_baseline leg of bench.py)."""
+    emis = np.ascontiguousarray(emis, dtype=np.float32)
+    T, B, V = emis.shape
+    return float(lib().oracle_ctc_time(emis.ctypes.data, T, B, V, beam, blank, int(is_log), nthreads))
+
+
+def synthetic_emissions(T: int, B: int, V: int, seed0: int = SEED0, sigma: float = 3.0,
+                        first: int = 0, log: bool = False) -> np.ndarray:
+    """[T][B][V] fp32 softmax(N(0, sigma^2) logits), computed in fp64.
+
+    Utterance u (global index first + b) draws from its own generator
+    default_rng(seed0 + u), so any shard of utterances reproduces exactly the
+    rows of the full batch."""
+    out = np.empty((T, B, V), np.float32)
+    for b in range(B):
+        rng = np.random.default_rng(seed0 + first + b)
+        z = rng.normal(0.0, sigma, size=(T, V))
+        z -= z.max(axis=1, keepdims=True)
+        if log:
+            p = z - np.log(np.exp(z).sum(axis=1, keepdims=True))
+        else:
+            e = np.exp(z)
+            p = e / e.sum(axis=1, keepdims=True)
+        out[:, b, :] = p.astype(np.float32)
+    return out

@@ -1,0 +1,168 @@
+"""GPU numerics of the MFMA fp32 GEMM / Linear / RNN kernels.
+
+References: the reference's own known-answer tests (nn_test.cpp, 4 d.p.),
+a forward of the reference's PyTorch model (baseline/model.py, fixture), and
+plain PyTorch fp32 ops on the CPU for random shapes.  Tolerance for fp32
+kernels: |err| <= 2e-5 * (1 + |ref|) (K <= 512, unit-scale data).
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, asr
+
+pytestmark = pytest.mark.gpu
+ATOL = 2e-5
+
+
+def dm(a):
+    return asr.DeviceMatrix.from_numpy(np.asarray(a, np.float32))
+
+
+def close(got, ref, tol=ATOL):
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(np.asarray(got, np.float64) - ref)
+    assert np.all(err <= tol * (1.0 + np.abs(ref))), f"max err {err.max()}"
+
+
+def test_linear_kat_nn_test():
+    k = json.loads((GOLDEN / "nn_test_kat.json").read_text())["linear"]
+    lin = asr.Linear(k["M"], k["K"], k["N"], np.array(k["weight"]).reshape(k["K"], k["N"]),
+                     np.array(k["bias"]))
+    y = lin.forward(dm(np.array(k["input"]).reshape(k["M"], k["K"]))).toCpu()
+    assert np.abs(y.flatten() - np.array(k["expected_4dp"])).max() < 6e-5
+
+
+def test_rnn_kat_nn_test():
+    k = json.loads((GOLDEN / "nn_test_kat.json").read_text())["rnn"]
+    T, B, I, H = k["T"], k["B"], k["in"], k["H"]
+    rnn = asr.RNN(B, I, H, T, 1, [(np.array(k["w_ih"]).reshape(I, H), np.array(k["w_hh"]).reshape(H, H),
+                                   np.array(k["b_ih"]), np.array(k["b_hh"]))])
+    y = rnn.forward(dm(np.array(k["input"]).reshape(T * B, I))).toCpu()
+    assert np.abs(y.flatten() - np.array(k["expected_4dp"])).max() < 6e-5
+
+
+def test_deepspeech_e2e_fixture():
+    """MLP x3 -> RNN -> MLP -> Linear + log_softmax == baseline/model.py forward."""
+    g = json.loads((GOLDEN / "deepspeech_e2e.json").read_text())
+    T, B = g["T"], g["B"]
+    x = dm(np.array(g["input_tm"]).reshape(T * B, g["features"]))
+    for L in g["mlp123"]:
+        lin = asr.Linear(T * B, L["in"], L["out"], np.array(L["w"]).reshape(L["in"], L["out"]), np.array(L["b"]))
+        x = lin.forward(x)
+        x = dm(x.toCpu())   # keep the layer's output alive independently of the layer object
+    r = g["rnn"]
+    H = r["H"]
+    rnn = asr.RNN(B, x.cols, H, T, 1, [(np.array(r["w_ih"]).reshape(x.cols, H), np.array(r["w_hh"]).reshape(H, H),
+                                        np.array(r["b_ih"]), np.array(r["b_hh"]))])
+    x = dm(rnn.forward(x).toCpu())
+    L5, L6 = g["mlp56"]
+    l5 = asr.Linear(T * B, L5["in"], L5["out"], np.array(L5["w"]).reshape(L5["in"], L5["out"]), np.array(L5["b"]))
+    x = dm(l5.forward(x).toCpu())
+    l6 = asr.Linear(T * B, L6["in"], L6["out"], np.array(L6["w"]).reshape(L6["in"], L6["out"]), np.array(L6["b"]),
+                    epilogue=asr.EPI_BIAS_LOGSOFTMAX)
+    y = l6.forward(x).toCpu()
+    close(y.flatten(), g["expected_logprobs_tm"], 5e-5)
+
+
+@pytest.mark.parametrize("M,K,N", [(27, 10, 40), (64, 256, 29), (1000, 256, 256), (33, 7, 65),
+                                   (128, 5, 3), (200, 512, 64), (3, 1, 1)])
+@pytest.mark.parametrize("epi", ["none", "bias", "relu"])
+def test_linear_random(M, K, N, epi):
+    rng = np.random.default_rng(M * 7 + K * 3 + N)
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = (rng.uniform(-1, 1, (K, N)) / np.sqrt(K)).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, N).astype(np.float32)
+    ref = torch.from_numpy(x) @ torch.from_numpy(W)
+    code = {"none": asr.EPI_NONE, "bias": asr.EPI_BIAS, "relu": asr.EPI_BIAS_RELU}[epi]
+    if epi != "none":
+        ref = ref + torch.from_numpy(b)
+    if epi == "relu":
+        ref = torch.relu(ref)
+    y = asr.DeviceMatrix(M, N)
+    asr.linear_fwd(dm(x), dm(W), dm(b.reshape(N, 1)), y, code)
+    close(y.toCpu(), ref.numpy())
+
+
+@pytest.mark.parametrize("M,K,N", [(32000, 256, 29), (100, 64, 5), (77, 30, 64)])
+def test_linear_logsoftmax(M, K, N):
+    rng = np.random.default_rng(N)
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = (rng.uniform(-1, 1, (K, N)) * 2 / np.sqrt(K)).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, N).astype(np.float32)
+    ref = torch.log_softmax(torch.from_numpy(x) @ torch.from_numpy(W) + torch.from_numpy(b), dim=1)
+    y = asr.DeviceMatrix(M, N)
+    asr.linear_fwd(dm(x), dm(W), dm(b.reshape(N, 1)), y, asr.EPI_BIAS_LOGSOFTMAX)
+    close(y.toCpu(), ref.numpy())
+
+
+def test_matmul_transposes_and_add():
+    rng = np.random.default_rng(3)
+    L = asr.lib()
+    M, K, N = 37, 19, 23
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    y = rng.standard_normal((M, N)).astype(np.float32)
+    dx, dy = dm(x), dm(y)   # keep the device buffers alive across the raw calls
+    z = asr.DeviceMatrix(K, N)
+    asr.check(L.asr_matmul_ta(dx.ptr, dy.ptr, z.ptr, M, K, N, None), "ta")
+    close(z.toCpu(), x.T.astype(np.float64) @ y)
+    y2 = rng.standard_normal((N, K)).astype(np.float32)
+    dy2 = dm(y2)
+    z2 = asr.DeviceMatrix(M, N)
+    asr.check(L.asr_matmul_tb(dx.ptr, dy2.ptr, z2.ptr, M, K, N, None), "tb")
+    close(z2.toCpu(), x.astype(np.float64) @ y2.T)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    da = dm(a)
+    c = asr.DeviceMatrix(M, K)
+    asr.check(L.asr_matadd(dx.ptr, da.ptr, c.ptr, M, K, -0.5, None), "add")
+    close(c.toCpu(), x + np.float32(-0.5) * a, 1e-6)
+
+
+def _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0=None):
+    H = w_hh.shape[0]
+    rnn = torch.nn.RNN(w_ih.shape[0], H, 1)
+    with torch.no_grad():
+        rnn.weight_ih_l0.copy_(torch.from_numpy(w_ih.T))
+        rnn.weight_hh_l0.copy_(torch.from_numpy(w_hh.T))
+        rnn.bias_ih_l0.copy_(torch.from_numpy(b_ih))
+        rnn.bias_hh_l0.copy_(torch.from_numpy(b_hh))
+        out, _ = rnn(torch.from_numpy(x.reshape(T, B, -1)),
+                     None if h0 is None else torch.from_numpy(h0.reshape(1, B, H)))
+    return out.reshape(T * B, H).numpy()
+
+
+@pytest.mark.parametrize("T,B,I,H", [(50, 64, 256, 256), (20, 3, 10, 50), (9, 5, 40, 128),
+                                     (12, 4, 24, 300), (6, 2, 8, 1)])
+def test_rnn_forward(T, B, I, H):
+    rng = np.random.default_rng(H)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    hid = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dm(x), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B)
+    close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 5e-5)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    asr.rnn_fwd(dm(x), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B,
+                h0=dm(h0))
+    close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 5e-5)
+
+
+def test_rnn_cell_forward():
+    rng = np.random.default_rng(5)
+    B, I, H = 17, 33, 70
+    x = rng.uniform(-1, 1, (B, I)).astype(np.float32)
+    h = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    w_ih = rng.uniform(-0.2, 0.2, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-0.2, 0.2, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    out = asr.DeviceMatrix(B, H)
+    asr.rnn_cell_fwd(dm(x), dm(h), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), out)
+    ref = torch.tanh((torch.from_numpy(x) @ torch.from_numpy(w_ih) + torch.from_numpy(h) @ torch.from_numpy(w_hh))
+                     + (torch.from_numpy(b_hh) + torch.from_numpy(b_ih)))
+    close(out.toCpu(), ref.numpy(), 5e-5)

@@ -1,0 +1,129 @@
+"""CPU tests of the parity oracle (oracle/ctc_oracle.cpp) — no GPU needed.
+
+Pins the restatement of /root/reference/CTCBeamSearch.cpp three ways:
+golden values of the reference's own test vector (main.cpp:51-60),
+exhaustive CTC enumeration (no pruning => exact prefix probabilities), and
+agreement with the literal fp32 probability-domain arithmetic at short T.
+"""
+import itertools
+import json
+import math
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, oracle
+
+
+def _collapse(path, blank):
+    out, prev = [], None
+    for s in path:
+        if s != prev and s != blank:
+            out.append(s)
+        prev = s
+    return tuple(out)
+
+
+def brute_force(emis, blank):
+    """Exact P(prefix) for one utterance by enumerating all V^T alignments."""
+    T, V = emis.shape
+    le = np.log(emis.astype(np.float64))
+    acc = {}
+    for path in itertools.product(range(V), repeat=T):
+        lp = float(sum(le[t, s] for t, s in enumerate(path)))
+        q = _collapse(path, blank)
+        acc.setdefault(q, []).append(lp)
+    return {q: float(np.logaddexp.reduce(v)) for q, v in acc.items()}
+
+
+def test_main_cpp_golden():
+    g = json.loads((GOLDEN / "main_cpp_ctc.json").read_text())
+    emis = np.array(g["emissions"], np.float32).reshape(g["T"], 1, g["V"])
+    codes = [ord(c) for c in g["vocab"]]
+    got = oracle.decode(emis, g["beam"], g["blank"], codes)[0]
+    s = lambda lab: "".join(g["vocab"][i] for i in lab)
+    assert [s(l) for l, _ in got] == [x[0] for x in g["expected_log"]]
+    for (l, lp), (_, e) in zip(got, g["expected_log"]):
+        assert lp == pytest.approx(e, abs=1e-12)
+    # compiled fixed reference gave cbacbc / -5.681380 / 0.0034088497
+    assert s(got[0][0]) == g["survey_A6"]["best"]
+    assert got[0][1] == pytest.approx(g["survey_A6"]["logp"], abs=5e-6)
+    prob = oracle.decode(emis, g["beam"], g["blank"], codes, prob_domain=True)[0]
+    assert prob[0][1] == pytest.approx(g["survey_A6"]["prob"], rel=1e-7)
+    assert [s(l) for l, _ in prob] == g["survey_A6"]["beam"]
+
+
+@pytest.mark.parametrize("T,V,seed", [(1, 4, 0), (2, 3, 1), (4, 4, 2), (6, 3, 3), (6, 4, 4), (5, 5, 5)])
+def test_exhaustive_enumeration(T, V, seed):
+    """With a beam wider than the state space the decoder is exact."""
+    rng = np.random.default_rng(seed)
+    e = rng.random((T, V)).astype(np.float32) + 0.05
+    e /= e.sum(1, keepdims=True)
+    exact = brute_force(e.astype(np.float64), blank=0)
+    got = oracle.decode(e.reshape(T, 1, V), beam=10 ** 6, blank=0, max_hyps=10 ** 4)[0]
+    assert len(got) == len(exact)
+    for lab, lp in got:
+        assert lp == pytest.approx(exact[tuple(lab)], abs=1e-9)
+
+
+@pytest.mark.parametrize("blank", [0, 2])
+def test_exhaustive_nonzero_blank(blank):
+    rng = np.random.default_rng(11)
+    T, V = 5, 4
+    e = rng.dirichlet(np.ones(V), size=T).astype(np.float32)
+    exact = brute_force(e.astype(np.float64), blank=blank)
+    got = oracle.decode(e.reshape(T, 1, V), beam=10 ** 6, blank=blank, max_hyps=10 ** 4)[0]
+    assert {tuple(l): lp for l, lp in got} == pytest.approx(exact, abs=1e-9)
+
+
+@pytest.mark.parametrize("T,V,beam,seed", [(12, 5, 3, 0), (20, 29, 10, 1), (30, 8, 6, 2)])
+def test_log_domain_matches_prob_domain(T, V, beam, seed):
+    """The log-domain restatement ranks like the reference's fp32 products."""
+    emis = oracle.synthetic_emissions(T, 3, V, seed0=100 + seed, sigma=2.0)
+    lg = oracle.decode(emis, beam, 0)
+    pr = oracle.decode(emis, beam, 0, prob_domain=True)
+    for a, b in zip(lg, pr):
+        assert [l for l, _ in a] == [l for l, _ in b]
+        for (_, x), (_, p) in zip(a, b):
+            assert math.exp(x) == pytest.approx(p, rel=2e-4)
+
+
+def test_prune_keeps_ties():
+    """F2/F1: all states tied at the cutoff survive (uniform emissions)."""
+    T, V, beam = 3, 3, 2
+    emis = np.full((T, 1, V), 1.0 / V, np.float32)
+    got = oracle.decode(emis, beam, 0)[0]
+    assert len(got) >= beam + 1
+    lg = oracle.decode(emis, 100, 0)[0]   # unpruned
+    assert len(lg) >= len(got)
+
+
+def test_beam_at_least_vocab():
+    """beam >= V: the literal reference threw at t=0 (cpp:107); F2 keeps all."""
+    emis = oracle.synthetic_emissions(5, 2, 4)
+    got = oracle.decode(emis, beam=500, blank=0)
+    exact = [brute_force(emis[:, b, :].astype(np.float64), 0) for b in range(2)]
+    for g, ex in zip(got, exact):
+        assert {tuple(l): lp for l, lp in g} == pytest.approx(ex, abs=1e-9)
+
+
+def test_zero_probabilities():
+    """Exact zeros give -inf scores that still count as states (prob 0)."""
+    emis = oracle.synthetic_emissions(6, 2, 5)
+    emis[2, :, 3] = 0.0
+    emis[:, 1, 1] = 0.0
+    got = oracle.decode(emis, beam=3, blank=0)
+    assert all(len(g) >= 1 for g in got)
+
+
+def test_synthetic_shard_invariance():
+    full = oracle.synthetic_emissions(5, 6, 7)
+    part = oracle.synthetic_emissions(5, 3, 7, first=3)
+    assert np.array_equal(full[:, 3:, :], part)
+
+
+def test_threads_deterministic():
+    emis = oracle.synthetic_emissions(40, 8, 29)
+    a = oracle.decode(emis, 10, 0, nthreads=1)
+    b = oracle.decode(emis, 10, 0, nthreads=4)
+    assert a == b
