@@ -25,7 +25,8 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libasr_amd.so"
+# ASR_LIB selects a diagnostic variant (e.g. libasr_amd_stamps.so) for tools/.
+LIB_PATH = PKG_DIR / os.environ.get("ASR_LIB", "libasr_amd.so")
 
 ASR_OK = 0
 ASR_ERR_ARG = 1

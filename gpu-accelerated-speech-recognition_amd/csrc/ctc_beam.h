@@ -29,9 +29,16 @@ struct CtcArgs {
     int* best_lab;          // [B][T] reversed labels of the best hypothesis
     int* best_len;          // [B]
     double* best_score;     // [B]
+    uint64_t* stamps;       // [B][8] phase clocks (diagnostic build only)
 };
 
 size_t ctc_lds_bytes(const CtcGeom& g);
+int ctc_launch_decode_v8(const CtcArgs& a, int waves, int rpt, hipStream_t s);
+int ctc_launch_decode_v32(const CtcArgs& a, int waves, int rpt, hipStream_t s);
+int ctc_launch_decode_v64(const CtcArgs& a, int waves, int rpt, hipStream_t s);
+int ctc_set_max_lds_v8();
+int ctc_set_max_lds_v32();
+int ctc_set_max_lds_v64();
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, hipStream_t s);
 int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);

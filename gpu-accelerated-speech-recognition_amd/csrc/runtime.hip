@@ -228,11 +228,20 @@ struct asr_ctc {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     asr::CtcArgs args{};
+    uint64_t* d_stamps = nullptr;   // diagnostic build only
+    int cap_stamps = 0;
 };
 
 namespace {
 
-int auto_waves(int K) { return K <= 64 ? 1 : (K <= 160 ? 2 : 4); }
+int auto_waves(int K) { (void)K; return 4; }
+
+// A (waves, vocab class, rows/thread) combination that ctc_beam_v*.hip instantiates.
+int valid_waves(const asr_ctc* h, int waves) {
+    if (h->kcap > 128) return 4;             // 4 rows per thread only with 4 waves
+    if (h->V + 1 > 32 && waves == 1) return 2;
+    return waves;
+}
 
 asr::CtcGeom plan(const asr_ctc* h, int waves) {
     asr::CtcGeom g{};
@@ -318,9 +327,12 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     h->blank_less = 0;
     for (int v = 0; v < V; v++)
         if (h->codes[blank_id] < h->codes[v]) h->blank_less |= 1ull << v;
-    int kcap = max_states > 0 ? max_states : h->K + std::max(16, h->K / 4);
+    // Automatic capacity: K plus room for ties at the cutoff; an overflow is
+    // detected on the device and the decode is re-run with more room.
+    int kcap = max_states > 0 ? max_states : h->K + std::max(8, h->K / 8);
     if (kcap < h->K) { delete h; return ASR_ERR_ARG; }
     kcap = (kcap + 31) & ~31;
+    if (kcap > 256) { delete h; return ASR_ERR_UNSUPPORTED; }
     h->kcap = kcap;
     h->waves_override = 0;
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
@@ -359,7 +371,7 @@ int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
 
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes) {
     if (!h) return ASR_ERR_ARG;
-    const int w = h->waves_override ? h->waves_override : auto_waves(h->K);
+    const int w = valid_waves(h, h->waves_override ? h->waves_override : auto_waves(h->K));
     if (max_states) *max_states = h->kcap;
     if (waves) *waves = w;
     if (lds_bytes) *lds_bytes = (int)asr::ctc_lds_bytes(plan(h, w));
@@ -370,7 +382,7 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     if (!h || !d_emis || T < 1 || B < 1) return ASR_ERR_ARG;
     int rc = ensure_ws(h, B, T);
     if (rc) return rc;
-    const int waves = h->waves_override ? h->waves_override : auto_waves(h->K);
+    const int waves = valid_waves(h, h->waves_override ? h->waves_override : auto_waves(h->K));
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
@@ -386,6 +398,14 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     a.best_lab = h->d_best_lab;
     a.best_len = h->d_best_len;
     a.best_score = h->d_best_score;
+#ifdef ASR_CTC_STAMPS
+    if (h->cap_stamps < B) {
+        hipFree(h->d_stamps);
+        ASR_HIP_TRY(hipMalloc(&h->d_stamps, sizeof(uint64_t) * 8 * B));
+        h->cap_stamps = B;
+    }
+    a.stamps = h->d_stamps;
+#endif
     const hipStream_t st = asr_stream(s);
     ASR_HIP_TRY(hipEventRecord(h->ev0, st));
     rc = asr::ctc_launch_decode(a, waves, st);
@@ -486,6 +506,16 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
     }
     return overflow ? ASR_ERR_BEAM_OVERFLOW : ASR_OK;
 }
+
+#ifdef ASR_CTC_STAMPS
+// Diagnostic build only: per-utterance phase clocks of the last decode.
+int asr_debug_ctc_stamps(asr_ctc_t* h, uint64_t* out) {
+    if (!h || !out || !h->have) return ASR_ERR_ARG;
+    ASR_HIP_TRY(hipStreamSynchronize(h->stream));
+    ASR_HIP_TRY(hipMemcpy(out, h->d_stamps, sizeof(uint64_t) * 8 * h->lastB, hipMemcpyDeviceToHost));
+    return ASR_OK;
+}
+#endif
 
 int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms) {
     if (!h || !ms) return ASR_ERR_ARG;

@@ -1,0 +1,63 @@
+"""Decoder timing sweep (waves per utterance x workload) and, with
+ASR_LIB=libasr_amd_stamps.so, the per-phase shader-clock breakdown.
+
+    python tools/ctc_profile.py            # timings
+    ASR_LIB=libasr_amd_stamps.so python tools/ctc_profile.py --stamps
+"""
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from __graft_entry__ import PKG, _load  # noqa: E402
+
+asr = _load("asr_amd", PKG / "asr_amd.py")
+oracle = _load("ctc_oracle", ROOT / "oracle" / "ctc_oracle.py")
+
+PHASES = ["chunk", "log+clear", "hash+links", "candidates", "select", "compact", "-", "-"]
+
+
+def run(T, B, V, beam, sigma, waves, reps, stamps):
+    emis = oracle.synthetic_emissions(T, B, V, sigma=sigma)
+    dec = asr.CTCDecoder(V, beam, 0, waves=waves)
+    ms = []
+    for _ in range(reps):
+        dec.decode(emis)
+        dec.best()
+        ms.append(dec.last_kernel_ms())
+    out = {"T": T, "B": B, "V": V, "beam": beam, "sigma": sigma, "waves": dec.config()[1],
+           "lds": dec.config()[2], "kernel_ms_min": round(min(ms), 4),
+           "us_per_frame_step": round(1e3 * min(ms) / T, 3)}
+    if stamps:
+        L = asr.lib()
+        buf = np.zeros((B, 8), np.uint64)
+        fn = L.asr_debug_ctc_stamps
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        asr.check(fn(dec.h, buf.ctypes.data), "stamps")
+        per = buf.astype(np.float64).mean(axis=0) / T
+        out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(6)}
+        out["cycles_total"] = round(per[:6].sum(), 1)
+    dec.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    asr.set_device(0)
+    cases = [(500, 64, 29, 50), (1000, 256, 29, 100), (1000, 256, 29, 50)]
+    for (T, B, V, beam) in cases:
+        for sigma in (3.0, 0.5):
+            for waves in (1, 2, 4):
+                print(json.dumps(run(T, B, V, beam, sigma, waves, args.reps, args.stamps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
