@@ -68,14 +68,15 @@ def make_inputs(T, B, In, H, V, first, seed=20261015):
     return x.reshape(T * B, In), (w_ih, w_hh, b_ih, b_hh), (w_out, b_out)
 
 
-def load_traffic(kernel_prefix: str):
-    """Measured HBM bytes per decode launch from the committed PMC profile."""
+def load_traffic(kernel: str):
+    """Measured HBM bytes per launch of `kernel` (rocprofv3 FETCH_SIZE +
+    WRITE_SIZE passes, summarised by tools/traffic_from_pmc.py into the
+    committed profiles/traffic.json); None when not profiled."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text())
-        return d.get(kernel_prefix)
+        return json.loads(p.read_text())[kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
 

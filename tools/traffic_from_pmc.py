@@ -1,0 +1,41 @@
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/traffic.json
+(HBM bytes per launch of each kernel), which bench.py embeds as roofline.traffic.
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md:
+FETCH_SIZE reads exactly half the bytes of 16-B/lane coalesced streaming
+reads; the decoder's emission loads are 4-B/lane global_load_dword, for
+which the counter is not halved (checked: 4055 KiB vs 3.71 MB of emission
+rows per C2 launch), so no correction is applied to the decoder.
+
+    python tools/traffic_from_pmc.py FETCH.csv WRITE.csv [source-label]
+"""
+import csv
+import json
+import sys
+from pathlib import Path
+
+
+def per_kernel(path):
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"]
+        short = name.split("(")[0].replace("void ", "").replace("asr::", "")
+        short = short.split("<")[0]
+        agg.setdefault(short, []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    fetch, write = per_kernel(sys.argv[1]), per_kernel(sys.argv[2])
+    label = sys.argv[3] if len(sys.argv) > 3 else ""
+    out = {}
+    for k in sorted(set(fetch) & set(write)):
+        out[k] = {"fetch_kib": round(fetch[k], 1), "write_kib": round(write[k], 1),
+                  "hbm_bytes_per_launch": int((fetch[k] + write[k]) * 1024), "source": label}
+    p = Path(__file__).resolve().parents[1] / "profiles" / "traffic.json"
+    p.write_text(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
