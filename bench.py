@@ -45,6 +45,15 @@ def shard_first(rank: int, per_rank: int) -> int:
     return rank * per_rank
 
 
+def reduce_max_over_ranks(x: float, world: int) -> float:
+    """Max of x over ranks (the job ends when the slowest rank ends)."""
+    if world <= 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def algorithmic_bytes_per_frame(V: int, beam: int) -> int:
     """4V (emission row, fp32, read once) + 32K (16-B beam
     record read + written) + 8K (8-B traceback record), K = beam + 1."""
@@ -142,10 +151,8 @@ def main():
         labels, lp = step()
     asr.synchronize()
     elapsed = time.perf_counter() - t0
+    elapsed = reduce_max_over_ranks(elapsed, world)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         dist.barrier()
 
     frames = world * B * T * args.steps
