@@ -35,6 +35,7 @@ ASR_ERR_OOM = 3
 ASR_ERR_BEAM_OVERFLOW = 4
 ASR_ERR_UNSUPPORTED = 5
 ASR_ERR_STATE = 6
+ASR_ERR_INTERNAL = 7
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_LOGSOFTMAX = 0, 1, 2, 3
 

@@ -16,6 +16,7 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
     const double* sc = a.fin_score + (size_t)b * kcap;
     const int* fn = a.fin_node + (size_t)b * kcap;
     const int2* nodes = a.nodes + (size_t)b * a.T * kcap;
+    const int nmax = a.T * kcap;
     int* out = a.best_lab + (size_t)b * a.T;
 
     uint64_t best = 0ull;
@@ -33,23 +34,28 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
         // Compare strings of slots i and bi from the front: materialise both
         // (reversed) then compare; ties are rare, this path is cold.
         int li = 0, lb = 0;
-        for (int x = fn[i]; x >= 0; x = nodes[x].x) li++;
-        for (int x = fn[bi]; x >= 0; x = nodes[x].x) lb++;
+        for (int x = fn[i]; x >= 0 && x < nmax && li < a.T; x = nodes[x].x) li++;
+        for (int x = fn[bi]; x >= 0 && x < nmax && lb < a.T; x = nodes[x].x) lb++;
         // k-th symbol from the front of slot s: walk (len-1-k) parents.
         bool less = false, decided = false;
         const int lmin = li < lb ? li : lb;
         for (int k = 0; k < lmin && !decided; k++) {
             int xi = fn[i], xb = fn[bi];
-            for (int s = 0; s < li - 1 - k; s++) xi = nodes[xi].x;
-            for (int s = 0; s < lb - 1 - k; s++) xb = nodes[xb].x;
-            const int ci = codes[nodes[xi].y], cb = codes[nodes[xb].y];
+            for (int s = 0; s < li - 1 - k && xi >= 0; s++) xi = nodes[xi].x;
+            for (int s = 0; s < lb - 1 - k && xb >= 0; s++) xb = nodes[xb].x;
+            if (xi < 0 || xb < 0) break;
+            const unsigned yi = (unsigned)nodes[xi].y, yb = (unsigned)nodes[xb].y;
+            const int ci = yi < (unsigned)a.g.V ? codes[yi] : 0;
+            const int cb = yb < (unsigned)a.g.V ? codes[yb] : 0;
             if (ci != cb) { less = ci < cb; decided = true; }
         }
         if (!decided) less = li < lb;
         if (less) bi = i;
     }
     int len = 0;
-    for (int x = fn[bi]; x >= 0; x = nodes[x].x) {
+    // Links always point to earlier frames, so a chain has at most T nodes;
+    // the bounds only guard against a corrupted table (never expected).
+    for (int x = fn[bi]; x >= 0 && x < nmax && len < a.T; x = nodes[x].x) {
         const int2 e = nodes[x];
         out[len++] = e.y;
     }
@@ -70,10 +76,11 @@ __global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, in
     const int n = a.fin_n[b];
     const int* fn = a.fin_node + (size_t)b * kcap;
     const int2* nodes = a.nodes + (size_t)b * a.T * kcap;
+    const int nmax = a.T * kcap;
     for (int i = threadIdx.x; i < n; i += 64) {
         int* out = all_lab + ((size_t)b * kcap + i) * a.T;
         int len = 0;
-        for (int x = fn[i]; x >= 0; x = nodes[x].x) out[len++] = nodes[x].y;
+        for (int x = fn[i]; x >= 0 && x < nmax && len < a.T; x = nodes[x].x) out[len++] = nodes[x].y;
         for (int p = 0, q = len - 1; p < q; p++, q--) {
             const int tmp = out[p];
             out[p] = out[q];

@@ -35,6 +35,7 @@ const char* asr_status_string(int status) {
         case ASR_ERR_BEAM_OVERFLOW: return "beam overflow: more tied survivors than max_states";
         case ASR_ERR_UNSUPPORTED: return "unsupported shape";
         case ASR_ERR_STATE: return "invalid call order";
+        case ASR_ERR_INTERNAL: return "internal decoder self-check failed";
         default: return "unknown status";
     }
 }
@@ -230,6 +231,10 @@ struct asr_ctc {
     asr::CtcArgs args{};
     uint64_t* d_stamps = nullptr;   // diagnostic build only
     int cap_stamps = 0;
+    bool auto_cap = true;           // max_states chosen by the library
+    asr_ctc* wide = nullptr;        // re-decode handle for tie overflow
+    const float* last_emis = nullptr;
+    int last_is_log = 0;
 };
 
 namespace {
@@ -238,7 +243,8 @@ int auto_waves(int K) { (void)K; return 4; }
 
 // A (waves, vocab class, rows/thread) combination that ctc_beam_v*.hip instantiates.
 int valid_waves(const asr_ctc* h, int waves) {
-    if (h->kcap > 128) return 4;             // 4 rows per thread only with 4 waves
+    if (h->V + 1 <= 8 && waves == 8) return 4;   // 8 waves need >= 2 columns per thread
+    if (h->kcap > 128 && waves < 4) return 4;   // 4 rows per thread only with 4 or 8 waves
     if (h->V + 1 > 32 && waves == 1) return 2;
     return waves;
 }
@@ -304,6 +310,15 @@ bool code_less(const asr_ctc* h, const int* a, int la, const int* b, int lb) {
     return la < lb;
 }
 
+// Status word of an utterance: bit 0 = beam overflow, bit 1 = self-check.
+int status_code(const int* status, int B) {
+    int any = 0;
+    for (int b = 0; b < B; b++) any |= status[b];
+    if (any & 2) return ASR_ERR_INTERNAL;
+    if (any & 1) return ASR_ERR_BEAM_OVERFLOW;
+    return ASR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -329,6 +344,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
         if (h->codes[blank_id] < h->codes[v]) h->blank_less |= 1ull << v;
     // Automatic capacity: K plus room for ties at the cutoff; an overflow is
     // detected on the device and the decode is re-run with more room.
+    h->auto_cap = max_states <= 0;
     int kcap = max_states > 0 ? max_states : h->K + std::max(8, h->K / 8);
     if (kcap < h->K) { delete h; return ASR_ERR_ARG; }
     kcap = (kcap + 31) & ~31;
@@ -336,7 +352,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     h->kcap = kcap;
     h->waves_override = 0;
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
-    if (asr::ctc_lds_bytes(plan(h, 4)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
+    if (asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }
     if (hipGetDevice(&h->device) != hipSuccess ||
@@ -357,6 +373,8 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     hipFree(h->d_codes);
     hipFree(h->d_all_lab);
     hipFree(h->d_all_len);
+    hipFree(h->d_stamps);
+    if (h->wide) asr_ctc_destroy(h->wide);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
     delete h;
@@ -364,7 +382,7 @@ int asr_ctc_destroy(asr_ctc_t* h) {
 }
 
 int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
-    if (!h || !(waves == 0 || waves == 1 || waves == 2 || waves == 4)) return ASR_ERR_ARG;
+    if (!h || !(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8)) return ASR_ERR_ARG;
     h->waves_override = waves;
     return ASR_OK;
 }
@@ -414,6 +432,8 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     rc = asr::ctc_launch_best(a, h->d_codes, st);
     if (rc) return rc;
     h->have = true;
+    h->last_emis = d_emis;
+    h->last_is_log = is_log ? 1 : 0;
     h->lastT = T;
     h->lastB = B;
     h->last_waves = waves;
@@ -433,19 +453,31 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
     ASR_HIP_TRY(hipMemcpy2DAsync(h->h_best_lab, sizeof(int) * ncol, h->d_best_lab, sizeof(int) * T,
                                  sizeof(int) * ncol, B, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipStreamSynchronize(st));
-    int overflow = 0;
+    const int stc = status_code(h->h_status, B);
+    if (stc == ASR_ERR_BEAM_OVERFLOW && h->auto_cap && h->kcap < 256) {
+        // More ties at the cutoff than room: decode again with twice the
+        // capacity (rare; exact results, never a silent truncation).
+        if (!h->wide) {
+            int rc = asr_ctc_create(h->codes.data(), h->V, h->beam, h->blank,
+                                    std::min(256, 2 * h->kcap), &h->wide);
+            if (rc) return rc;
+            h->wide->auto_cap = true;
+        }
+        int rc = asr_ctc_decode(h->wide, h->last_emis, T, B, h->last_is_log, h->stream);
+        if (rc) return rc;
+        return asr_ctc_get_best(h->wide, labels, max_len, lengths, logp);
+    }
     for (int b = 0; b < B; b++) {
         const int len = h->h_best_len[b];
         if (lengths) lengths[b] = len;
         if (logp) logp[b] = h->h_best_score[b];
-        overflow |= h->h_status[b];
         if (labels) {
             const int* fwd = h->h_best_lab + (size_t)b * ncol;
             const int n = std::min(len, max_len);
             for (int i = 0; i < n; i++) labels[(size_t)b * max_len + i] = fwd[i];
         }
     }
-    return overflow ? ASR_ERR_BEAM_OVERFLOW : ASR_OK;
+    return stc;
 }
 
 int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, int32_t* lengths,
@@ -475,10 +507,20 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
     ASR_HIP_TRY(hipMemcpyAsync(all_len.data(), h->d_all_len, sizeof(int) * B * kc, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(lab.data(), h->d_all_lab, sizeof(int) * need, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipStreamSynchronize(st));
-    int overflow = 0;
+    const int stc = status_code(status.data(), B);
+    if (stc == ASR_ERR_BEAM_OVERFLOW && h->auto_cap && h->kcap < 256) {
+        if (!h->wide) {
+            rc = asr_ctc_create(h->codes.data(), h->V, h->beam, h->blank, std::min(256, 2 * h->kcap),
+                                &h->wide);
+            if (rc) return rc;
+            h->wide->auto_cap = true;   // keeps doubling, up to 256 states
+        }
+        rc = asr_ctc_decode(h->wide, h->last_emis, T, B, h->last_is_log, st);
+        if (rc) return rc;
+        return asr_ctc_get_beams(h->wide, max_hyps, max_len, n_hyps, lengths, labels, logp);
+    }
     std::vector<std::vector<int>> fwd;
     for (int b = 0; b < B; b++) {
-        overflow |= status[b];
         const int n = fin_n[b];
         fwd.assign(n, {});
         std::vector<int> order(n);
@@ -504,7 +546,7 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
                     labels[base * max_len + x] = fwd[i][x];
         }
     }
-    return overflow ? ASR_ERR_BEAM_OVERFLOW : ASR_OK;
+    return stc;
 }
 
 #ifdef ASR_CTC_STAMPS

@@ -44,7 +44,8 @@ typedef enum asr_status {
     ASR_ERR_OOM = 3,            /* device or pinned host allocation failed */
     ASR_ERR_BEAM_OVERFLOW = 4,  /* more tied survivors than max_states     */
     ASR_ERR_UNSUPPORTED = 5,    /* shape outside what the kernels support  */
-    ASR_ERR_STATE = 6           /* call out of order (e.g. no decode yet)  */
+    ASR_ERR_STATE = 6,          /* call out of order (e.g. no decode yet)  */
+    ASR_ERR_INTERNAL = 7        /* a decoder self-check failed (a bug)     */
 } asr_status;
 
 const char* asr_status_string(int status);
@@ -136,8 +137,11 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
 /* Best hypothesis of each utterance (cpp:74-84: max score, first in string
  * order on ties).  Synchronises the decode stream.  h_labels[B][max_len]
  * (label ids), h_lengths[B], h_logp[B] (fp64 log-probability).
- * Returns ASR_ERR_BEAM_OVERFLOW if an utterance had more tied survivors than
- * max_states (its result is then not the reference's). */
+ * If an utterance had more tied survivors than max_states, the batch is
+ * decoded again with a wider beam capacity (up to 256 states) before
+ * returning; ASR_ERR_BEAM_OVERFLOW only if that is not enough (the result is
+ * then not the reference's) or if the handle was created with an explicit
+ * max_states. */
 int asr_ctc_get_best(asr_ctc_t* h, int32_t* h_labels, int max_len, int32_t* h_lengths,
                      double* h_logp);
 
@@ -150,7 +154,7 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps
 /* Device time of the last decode's beam-search kernel (ms, HIP events on the
  * decode stream) and its launch geometry; for roofline accounting. */
 int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms);
-/* Tuning knobs: waves per utterance (1, 2 or 4; 0 = automatic). */
+/* Tuning knobs: waves per utterance (1, 2, 4 or 8; 0 = automatic). */
 int asr_ctc_set_waves(asr_ctc_t* h, int waves);
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes);
 

@@ -63,7 +63,7 @@ def test_random_parity(T, B, V, beam):
     assert_beams_equal(gpu_beams(emis, beam), ref, f"T={T} B={B} V={V} beam={beam}")
 
 
-@pytest.mark.parametrize("waves", [1, 2, 4])
+@pytest.mark.parametrize("waves", [1, 2, 4, 8])
 def test_waves_bitwise_equal(waves):
     emis = oracle.synthetic_emissions(70, 8, 29, seed0=77)
     ref = oracle.decode(emis, 50, 0, nthreads=cpu_threads())
@@ -108,6 +108,8 @@ def test_ties_uniform_emissions():
 
 
 def test_overflow_is_reported():
+    """An explicit max_states too small for the ties is an error, never a
+    silently different beam."""
     T, V, beam = 6, 4, 3
     emis = np.full((T, 1, V), 1.0 / V, np.float32)
     dec = asr.CTCDecoder(V, beam, 0, max_states=4)
@@ -115,6 +117,19 @@ def test_overflow_is_reported():
     with pytest.raises(asr.AsrError) as e:
         dec.best()
     assert e.value.status == asr.ASR_ERR_BEAM_OVERFLOW
+
+
+def test_overflow_retried_with_automatic_capacity():
+    """With the automatic capacity, tie overflow re-decodes with more room."""
+    T, V, beam = 8, 4, 3
+    emis = np.full((T, 3, V), 1.0 / V, np.float32)
+    ref = oracle.decode(emis, beam, 0)
+    assert max(len(r) for r in ref) > 64   # two doublings of the default 32 states
+    dec = asr.CTCDecoder(V, beam, 0)
+    dec.decode(emis)
+    best, lp = dec.best()
+    assert best == [r[0][0] for r in ref]
+    assert_beams_equal(dec.beams(256), ref, "retry")
 
 
 def test_shard_invariance():

@@ -19,7 +19,7 @@ from __graft_entry__ import PKG, _load  # noqa: E402
 asr = _load("asr_amd", PKG / "asr_amd.py")
 oracle = _load("ctc_oracle", ROOT / "oracle" / "ctc_oracle.py")
 
-PHASES = ["chunk", "log+clear", "hash+links", "candidates", "select", "compact", "-", "-"]
+PHASES = ["chunk", "P0 links", "P1 cand", "P2a stage1", "P2b exact-lse", "P2c stage2", "P3 compact", "-"]
 
 
 def run(T, B, V, beam, sigma, waves, reps, stamps):
@@ -40,8 +40,8 @@ def run(T, B, V, beam, sigma, waves, reps, stamps):
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         asr.check(fn(dec.h, buf.ctypes.data), "stamps")
         per = buf.astype(np.float64).mean(axis=0) / T
-        out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(6)}
-        out["cycles_total"] = round(per[:6].sum(), 1)
+        out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(7)}
+        out["cycles_total"] = round(per[:7].sum(), 1)
     dec.close()
     return out
 
@@ -50,12 +50,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--waves", default="1,2,4")
     args = ap.parse_args()
+    global WAVES
+    WAVES = [int(x) for x in args.waves.split(",")]
     asr.set_device(0)
-    cases = [(500, 64, 29, 50), (1000, 256, 29, 100), (1000, 256, 29, 50)]
-    for (T, B, V, beam) in cases:
+    ap_cases = [(500, 64, 29, 50), (1000, 256, 29, 100)]
+    for (T, B, V, beam) in ap_cases:
         for sigma in (3.0, 0.5):
-            for waves in (1, 2, 4):
+            for waves in WAVES:
                 print(json.dumps(run(T, B, V, beam, sigma, waves, args.reps, args.stamps)), flush=True)
 
 
