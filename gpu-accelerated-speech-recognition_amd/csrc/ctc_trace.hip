@@ -52,6 +52,11 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
         if (!decided) less = li < lb;
         if (less) bi = i;
     }
+    if (bi < 0) {   // no final hypothesis (never expected: n >= 1)
+        a.best_len[b] = 0;
+        a.best_score[b] = -INFINITY;
+        return;
+    }
     int len = 0;
     // Links always point to earlier frames, so a chain has at most T nodes;
     // the bounds only guard against a corrupted table (never expected).

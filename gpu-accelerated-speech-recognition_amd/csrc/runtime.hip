@@ -239,7 +239,9 @@ struct asr_ctc {
 
 namespace {
 
-int auto_waves(int K) { (void)K; return 4; }
+// 8 waves per utterance measured fastest at C2/C3; valid_waves
+// lowers it where a narrower instantiation is required.
+int auto_waves(int K) { (void)K; return 8; }
 
 // A (waves, vocab class, rows/thread) combination that ctc_beam_v*.hip instantiates.
 int valid_waves(const asr_ctc* h, int waves) {
