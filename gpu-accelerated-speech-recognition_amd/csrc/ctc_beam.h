@@ -4,6 +4,8 @@
 
 namespace asr {
 
+constexpr int NSTAMP = 16;   // diagnostic phase clocks per utterance
+
 // Launch geometry of one decode, shared by the host planner and the kernel.
 struct CtcGeom {
     int V;       // labels incl. blank (<= 63)
@@ -12,7 +14,7 @@ struct CtcGeom {
     int kcap;    // slot/state capacity incl. ties at the cutoff
     int sb;      // log2 of the candidate row stride (row = V+1 columns)
     int ch;      // emission frames staged per prefetch chunk
-    int ht;      // hash-table cells (power of two >= 2*kcap)
+    int ht;      // orphan-group table cells (power of two >= 4*kcap, 8-cell buckets)
 };
 
 struct CtcArgs {
@@ -29,7 +31,7 @@ struct CtcArgs {
     int* best_lab;          // [B][T] reversed labels of the best hypothesis
     int* best_len;          // [B]
     double* best_score;     // [B]
-    uint64_t* stamps;       // [B][8] phase clocks (diagnostic build only)
+    uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
 };
 
 size_t ctc_lds_bytes(const CtcGeom& g);

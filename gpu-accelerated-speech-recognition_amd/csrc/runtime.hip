@@ -261,7 +261,7 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
     const int nt = 64 * waves;
     g.ch = std::max(1, std::min(32, 16 * nt / h->V));
     int ht = 64;
-    while (ht < 2 * h->kcap) ht <<= 1;
+    while (ht < 4 * h->kcap) ht <<= 1;
     g.ht = ht;
     return g;
 }
@@ -421,7 +421,7 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
 #ifdef ASR_CTC_STAMPS
     if (h->cap_stamps < B) {
         hipFree(h->d_stamps);
-        ASR_HIP_TRY(hipMalloc(&h->d_stamps, sizeof(uint64_t) * 8 * B));
+        ASR_HIP_TRY(hipMalloc(&h->d_stamps, sizeof(uint64_t) * asr::NSTAMP * B));
         h->cap_stamps = B;
     }
     a.stamps = h->d_stamps;
@@ -556,7 +556,7 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
 int asr_debug_ctc_stamps(asr_ctc_t* h, uint64_t* out) {
     if (!h || !out || !h->have) return ASR_ERR_ARG;
     ASR_HIP_TRY(hipStreamSynchronize(h->stream));
-    ASR_HIP_TRY(hipMemcpy(out, h->d_stamps, sizeof(uint64_t) * 8 * h->lastB, hipMemcpyDeviceToHost));
+    ASR_HIP_TRY(hipMemcpy(out, h->d_stamps, sizeof(uint64_t) * asr::NSTAMP * h->lastB, hipMemcpyDeviceToHost));
     return ASR_OK;
 }
 #endif

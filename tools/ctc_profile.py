@@ -19,7 +19,9 @@ from __graft_entry__ import PKG, _load  # noqa: E402
 asr = _load("asr_amd", PKG / "asr_amd.py")
 oracle = _load("ctc_oracle", ROOT / "oracle" / "ctc_oracle.py")
 
-PHASES = ["chunk", "P0 links", "P1 cand", "P2a stage1", "P2b exact-lse", "P2c stage2", "P3 compact", "-"]
+PHASES = ["chunk", "P1 cand", "P2a stage1", "P2b exact-lse", "P2c stage2", "P3a scan",
+          "P3b+barrier", "P3b max wave", "P3b max wave to desc", "loop:loads+hash", "loop:writes+newidx",
+          "loop:link/join", "loop:find", "-", "-", "-"]
 
 
 def run(T, B, V, beam, sigma, waves, reps, stamps):
@@ -35,12 +37,12 @@ def run(T, B, V, beam, sigma, waves, reps, stamps):
            "us_per_frame_step": round(1e3 * min(ms) / T, 3)}
     if stamps:
         L = asr.lib()
-        buf = np.zeros((B, 8), np.uint64)
+        buf = np.zeros((B, 16), np.uint64)
         fn = L.asr_debug_ctc_stamps
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         asr.check(fn(dec.h, buf.ctypes.data), "stamps")
         per = buf.astype(np.float64).mean(axis=0) / T
-        out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(7)}
+        out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(16) if PHASES[i] != "-"}
         out["cycles_total"] = round(per[:7].sum(), 1)
     dec.close()
     return out
