@@ -317,16 +317,24 @@ class CTCDecoder:
         check(lib().asr_memcpy_h2d(self._emis.ptr, _ptr(emis), emis.nbytes, stream), "asr_memcpy_h2d")
         self.decode_device(self._emis.ptr, T, B, is_log, stream)
 
-    def best(self, allow_overflow: bool = False) -> Tuple[List[List[int]], np.ndarray]:
-        """Best label sequence and fp64 log-prob of every utterance."""
+    def best_arrays(self, allow_overflow: bool = False) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Best hypotheses as arrays: labels [B][T] int32 (row b valid up to
+        lengths[b]), lengths [B], fp64 log-probs [B].  Reuses host buffers:
+        copy them before the next call if they must persist."""
         B, T = self.B, self.T
-        lab = np.zeros((B, T), np.int32)
-        ln = np.zeros(B, np.int32)
-        lp = np.zeros(B, np.float64)
-        rc = lib().asr_ctc_get_best(self.h, _ptr(lab), T, _ptr(ln), _ptr(lp))
+        if getattr(self, "_best_bufs", None) is None or self._best_bufs[0].shape != (B, max(T, 1)):
+            self._best_bufs = (np.zeros((B, max(T, 1)), np.int32), np.zeros(B, np.int32),
+                               np.zeros(B, np.float64))
+        lab, ln, lp = self._best_bufs
+        rc = lib().asr_ctc_get_best(self.h, _ptr(lab), max(T, 1), _ptr(ln), _ptr(lp))
         if not (allow_overflow and rc == ASR_ERR_BEAM_OVERFLOW):
             check(rc, "asr_ctc_get_best")
-        return [list(lab[b, :ln[b]]) for b in range(B)], lp
+        return lab, ln, lp
+
+    def best(self, allow_overflow: bool = False) -> Tuple[List[List[int]], np.ndarray]:
+        """Best label sequence and fp64 log-prob of every utterance."""
+        lab, ln, lp = self.best_arrays(allow_overflow)
+        return [lab[b, :ln[b]].tolist() for b in range(self.B)], lp.copy()
 
     def beams(self, max_hyps: int) -> List[List[Tuple[List[int], float]]]:
         """Ranked final beam (logp desc, string asc) of every utterance."""
@@ -337,7 +345,7 @@ class CTCDecoder:
         lp = np.zeros((B, max_hyps), np.float64)
         check(lib().asr_ctc_get_beams(self.h, max_hyps, max(T, 1), _ptr(nh), _ptr(ln), _ptr(lab),
                                       _ptr(lp)), "asr_ctc_get_beams")
-        return [[(list(lab[b, k, :ln[b, k]]), float(lp[b, k])) for k in range(min(nh[b], max_hyps))]
+        return [[(lab[b, k, :ln[b, k]].tolist(), float(lp[b, k])) for k in range(min(nh[b], max_hyps))]
                 for b in range(B)]
 
     def last_kernel_ms(self) -> float:

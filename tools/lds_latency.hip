@@ -73,6 +73,20 @@ __global__ void lat(uint64_t* out, int mode, int active_waves) {
         } else if (mode == 18) {    // ds_add_u32 no return, 16 addresses (histogram-like)
             for (int i = 0; i < N; i++) atomicAdd(&buf[(tid * 7) & 15], 1u);
             x = buf[1];
+        } else if (mode == 19) {    // ds_add_u32, 2 addresses x 32 lanes
+            for (int i = 0; i < N; i++) atomicAdd(&buf[tid & 1], 1u);
+            x = buf[1];
+        } else if (mode == 20) {    // ds_add_u32, 48 lanes one address + 16 distinct
+            for (int i = 0; i < N; i++) atomicAdd(&buf[(tid & 63) < 48 ? 0 : (tid & 63)], 1u);
+            x = buf[1];
+        } else if (mode == 21) {    // ds_add_u32, 20 active lanes, one address
+            if ((tid & 63) < 20)
+                for (int i = 0; i < N; i++) atomicAdd(&buf[0], 1u);
+            x = buf[1];
+        } else if (mode == 22) {    // ds_add_u32, 64 lanes, 8 addresses skewed (geometric)
+            const int a = __builtin_ctz((tid & 63) | 64);   // 0:32 lanes, 1:16, 2:8, ...
+            for (int i = 0; i < N; i++) atomicAdd(&buf[a], 1u);
+            x = buf[1];
         } else if (mode == 6) {     // dependent ds_read_b64
             uint64_t y = x;
             for (int i = 0; i < N; i++) y = b64[y & 1023] + (y & 1023);
@@ -94,8 +108,10 @@ int main() {
                            "ds_add_rtn same addr", "ds_add_rtn distinct", "ds_or_b64 same addr",
                            "ds_cmpst same addr", "ds_or_b32 same addr", "ds_or_b64 distinct",
                            "ds_max_u64 same addr", "ds_max_u32 same addr", "ds_or_b64 4/addr",
-                           "ds_add_u64 same addr", "ds_add_u32 same addr", "ds_add_u32 16 addrs"};
-    for (int mode = 16; mode < 19; mode++)
+                           "ds_add_u64 same addr", "ds_add_u32 same addr", "ds_add_u32 16 addrs",
+                           "ds_add_u32 2x32", "ds_add_u32 48+16", "ds_add_u32 20 lanes 1 addr",
+                           "ds_add_u32 geometric"};
+    for (int mode = 17; mode < 23; mode++)
         for (int nw : {1, 8}) {
             for (int rep = 0; rep < 2; rep++) {
                 hipLaunchKernelGGL(lat, dim3(64), dim3(64 * nw), 0, 0, d, mode,
