@@ -23,9 +23,10 @@ struct CtcArgs {
     int T, B;
     int is_log;
     uint64_t blank_less;    // bit c: code(blank) < code(c)
-    int2* nodes;            // [B][T*kcap] (parent node, label)
+    int4* nodes;            // [B][T*kcap] (parent node, 0, 8 labels packed lo, hi)
     int* fin_n;             // [B] final hypotheses
     int* fin_node;          // [B][kcap]
+    uint64_t* fin_tail;     // [B][kcap]  labels after fin_node's block (count << 56)
     double* fin_score;      // [B][kcap]
     int* status;            // [B] 1 = beam overflow
     int* best_lab;          // [B][T] reversed labels of the best hypothesis
@@ -42,7 +43,7 @@ int ctc_set_max_lds_v8();
 int ctc_set_max_lds_v32();
 int ctc_set_max_lds_v64();
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
-int ctc_launch_best(const CtcArgs& a, const int* d_codes, hipStream_t s);
+int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s);
 int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);
 int ctc_set_max_lds();
 

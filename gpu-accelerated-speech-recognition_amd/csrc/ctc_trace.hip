@@ -6,18 +6,48 @@ namespace asr {
 
 size_t ctc_lds_bytes(const CtcGeom& g) { return lds_plan(g).total; }
 
+// A hypothesis is (node, tail): the chain of 8-label blocks ending at node
+// (each record: parent node, 8 labels packed 8 bits each, first label lowest)
+// followed by the tail's labels.  Links always point to earlier frames, so a
+// chain has at most T/8 blocks; the bounds only guard a corrupted table.
+
+__device__ __forceinline__ uint32_t block_label(const int4 r, int k) {
+    const uint64_t pk = ((uint64_t)(uint32_t)r.w << 32) | (uint32_t)r.z;
+    return (uint32_t)(pk >> (8 * k)) & 0xFFu;
+}
+
+// Chase the block chain of `x` into ids[] (last block first); returns the
+// number of blocks.
+__device__ int chase_blocks(const int4* nodes, int nmax, int x, int* ids, int maxb) {
+    int nb = 0;
+    for (; x >= 0 && x < nmax && nb < maxb; x = nodes[x].x) ids[nb++] = x;
+    return nb;
+}
+
+// Label k (from the front) of a hypothesis whose blocks are ids[0..nb)
+// (last first) followed by tail.
+__device__ uint32_t label_at(const int4* nodes, const int* ids, int nb, uint64_t tail, int k) {
+    if (k < 8 * nb) return block_label(nodes[ids[nb - 1 - k / 8]], k % 8);
+    return (uint32_t)(tail >> (8 * (k - 8 * nb))) & 0xFFu;
+}
+
 // Best-path traceback: per utterance, the maximum final score; among ties the
 // smallest code string (std::map order, cpp:76-84).  Labels are written in
-// forward order to best_lab[b][T].
-__global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* codes) {
+// forward order to best_lab[b][T].  chain: [B][2][T/8+1] scratch.
+__global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* codes, int* chain) {
     const int b = blockIdx.x, lane = threadIdx.x;
     const int kcap = a.g.kcap;
     const int n = a.fin_n[b];
     const double* sc = a.fin_score + (size_t)b * kcap;
     const int* fn = a.fin_node + (size_t)b * kcap;
-    const int2* nodes = a.nodes + (size_t)b * a.T * kcap;
+    const uint64_t* ft = a.fin_tail + (size_t)b * kcap;
+    const int4* nodes = a.nodes + (size_t)b * a.T * kcap;
     const int nmax = a.T * kcap;
+    const int maxb = a.T / 8 + 1;
+    int* ids = chain + (size_t)b * 2 * maxb;   // best candidate's blocks
+    int* ids2 = ids + maxb;                    // challenger's (ties only)
     int* out = a.best_lab + (size_t)b * a.T;
+    __shared__ int s_nb, s_bi;
 
     uint64_t best = 0ull;
     for (int i = lane; i < n; i += 64) {
@@ -25,72 +55,88 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
         best = k > best ? k : best;
     }
     for (int o = 32; o > 0; o >>= 1) { uint64_t x = __shfl_xor(best, o); best = x > best ? x : best; }
-    if (lane != 0) return;
-    // Among ties (almost always one), keep the smallest code string.
-    int bi = -1;
-    for (int i = 0; i < n; i++) {
-        if (asr_d2key(sc[i]) != best) continue;
-        if (bi < 0) { bi = i; continue; }
-        // Compare strings of slots i and bi from the front: materialise both
-        // (reversed) then compare; ties are rare, this path is cold.
-        int li = 0, lb = 0;
-        for (int x = fn[i]; x >= 0 && x < nmax && li < a.T; x = nodes[x].x) li++;
-        for (int x = fn[bi]; x >= 0 && x < nmax && lb < a.T; x = nodes[x].x) lb++;
-        // k-th symbol from the front of slot s: walk (len-1-k) parents.
-        bool less = false, decided = false;
-        const int lmin = li < lb ? li : lb;
-        for (int k = 0; k < lmin && !decided; k++) {
-            int xi = fn[i], xb = fn[bi];
-            for (int s = 0; s < li - 1 - k && xi >= 0; s++) xi = nodes[xi].x;
-            for (int s = 0; s < lb - 1 - k && xb >= 0; s++) xb = nodes[xb].x;
-            if (xi < 0 || xb < 0) break;
-            const unsigned yi = (unsigned)nodes[xi].y, yb = (unsigned)nodes[xb].y;
-            const int ci = yi < (unsigned)a.g.V ? codes[yi] : 0;
-            const int cb = yb < (unsigned)a.g.V ? codes[yb] : 0;
-            if (ci != cb) { less = ci < cb; decided = true; }
+    if (lane == 0) {
+        // Among ties (almost always one), keep the smallest code string.
+        int bi = -1, nb = 0;
+        for (int i = 0; i < n; i++) {
+            if (asr_d2key(sc[i]) != best) continue;
+            if (bi < 0) {
+                bi = i;
+                nb = chase_blocks(nodes, nmax, fn[i], ids, maxb);
+                continue;
+            }
+            const int nb2 = chase_blocks(nodes, nmax, fn[i], ids2, maxb);
+            const int li = 8 * nb2 + (int)(ft[i] >> 56), lb = 8 * nb + (int)(ft[bi] >> 56);
+            const int lmin = li < lb ? li : lb;
+            bool less = li < lb, decided = false;
+            for (int k = 0; k < lmin && !decided; k++) {
+                const uint32_t yi = label_at(nodes, ids2, nb2, ft[i], k);
+                const uint32_t yb = label_at(nodes, ids, nb, ft[bi], k);
+                const int ci = yi < (unsigned)a.g.V ? codes[yi] : 0;
+                const int cb = yb < (unsigned)a.g.V ? codes[yb] : 0;
+                if (ci != cb) { less = ci < cb; decided = true; }
+            }
+            if (less) {   // the challenger becomes the best: keep its blocks
+                bi = i;
+                nb = nb2;
+                for (int j = 0; j < nb2; j++) ids[j] = ids2[j];
+            }
         }
-        if (!decided) less = li < lb;
-        if (less) bi = i;
+        s_nb = nb;
+        s_bi = bi;
     }
+    __syncthreads();
+    const int bi = s_bi, nb = s_nb;
     if (bi < 0) {   // no final hypothesis (never expected: n >= 1)
-        a.best_len[b] = 0;
-        a.best_score[b] = -INFINITY;
+        if (lane == 0) {
+            a.best_len[b] = 0;
+            a.best_score[b] = -INFINITY;
+        }
         return;
     }
-    int len = 0;
-    // Links always point to earlier frames, so a chain has at most T nodes;
-    // the bounds only guard against a corrupted table (never expected).
-    for (int x = fn[bi]; x >= 0 && x < nmax && len < a.T; x = nodes[x].x) {
-        const int2 e = nodes[x];
-        out[len++] = e.y;
+    const uint64_t tail = ft[bi];
+    const int nt = (int)(tail >> 56) < 8 ? (int)(tail >> 56) : 7;
+    const int len = 8 * nb + nt <= a.T ? 8 * nb + nt : a.T;
+    for (int j = lane; j < nb; j += 64) {   // block j from the front
+        const int4 r = nodes[ids[nb - 1 - j]];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (8 * j + k < len) out[8 * j + k] = (int)block_label(r, k);
     }
-    for (int i = 0, j = len - 1; i < j; i++, j--) {   // chased last-first: reverse
-        const int tmp = out[i];
-        out[i] = out[j];
-        out[j] = tmp;
+    if (lane < nt && 8 * nb + lane < len) out[8 * nb + lane] = (int)((tail >> (8 * lane)) & 0xFFu);
+    if (lane == 0) {
+        a.best_len[b] = len;
+        a.best_score[b] = sc[bi];
     }
-    a.best_len[b] = len;
-    a.best_score[b] = sc[bi];
 }
 
 // Full-beam traceback: every final hypothesis of every utterance, labels in
-// forward order into all_lab[b][slot][T].
+// forward order into all_lab[b][slot][T].  One lane per hypothesis: count
+// the blocks, then chase again writing each block at its final position.
 __global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, int* all_len) {
     const int b = blockIdx.x;
     const int kcap = a.g.kcap;
     const int n = a.fin_n[b];
     const int* fn = a.fin_node + (size_t)b * kcap;
-    const int2* nodes = a.nodes + (size_t)b * a.T * kcap;
+    const uint64_t* ft = a.fin_tail + (size_t)b * kcap;
+    const int4* nodes = a.nodes + (size_t)b * a.T * kcap;
     const int nmax = a.T * kcap;
+    const int maxb = a.T / 8 + 1;
     for (int i = threadIdx.x; i < n; i += 64) {
         int* out = all_lab + ((size_t)b * kcap + i) * a.T;
-        int len = 0;
-        for (int x = fn[i]; x >= 0 && x < nmax && len < a.T; x = nodes[x].x) out[len++] = nodes[x].y;
-        for (int p = 0, q = len - 1; p < q; p++, q--) {
-            const int tmp = out[p];
-            out[p] = out[q];
-            out[q] = tmp;
+        int nb = 0;
+        for (int x = fn[i]; x >= 0 && x < nmax && nb < maxb; x = nodes[x].x) nb++;
+        const uint64_t tail = ft[i];
+        const int nt = (int)(tail >> 56) < 8 ? (int)(tail >> 56) : 7;
+        const int len = 8 * nb + nt <= a.T ? 8 * nb + nt : a.T;
+        int j = nb - 1;
+        for (int x = fn[i]; x >= 0 && x < nmax && j >= 0; x = nodes[x].x, j--) {
+            const int4 r = nodes[x];
+            for (int k = 0; k < 8; k++)
+                if (8 * j + k < len) out[8 * j + k] = (int)block_label(r, k);
         }
+        for (int k = 0; k < nt; k++)
+            if (8 * nb + k < len) out[8 * nb + k] = (int)((tail >> (8 * k)) & 0xFFu);
         all_len[(size_t)b * kcap + i] = len;
     }
 }
@@ -104,8 +150,8 @@ int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s) {
     return ASR_ERR_UNSUPPORTED;
 }
 
-int ctc_launch_best(const CtcArgs& a, const int* d_codes, hipStream_t s) {
-    hipLaunchKernelGGL(ctc_best_kernel, dim3(a.B), dim3(64), 0, s, a, d_codes);
+int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s) {
+    hipLaunchKernelGGL(ctc_best_kernel, dim3(a.B), dim3(64), 0, s, a, d_codes, d_chain);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

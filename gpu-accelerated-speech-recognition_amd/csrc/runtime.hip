@@ -212,8 +212,10 @@ struct asr_ctc {
     int device;
     // workspace (device)
     int capB = 0, capT = 0;
-    int2* d_nodes = nullptr;
+    int4* d_nodes = nullptr;
     int *d_fin_n = nullptr, *d_fin_node = nullptr, *d_status = nullptr;
+    uint64_t* d_fin_tail = nullptr;
+    int* d_chain = nullptr;         // traceback scratch [B][2][T/8+1]
     double* d_fin_score = nullptr;
     int *d_best_lab = nullptr, *d_best_len = nullptr;
     double* d_best_score = nullptr;
@@ -268,6 +270,8 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
 
 void free_ws(asr_ctc* h) {
     hipFree(h->d_nodes); hipFree(h->d_fin_n); hipFree(h->d_fin_node); hipFree(h->d_status);
+    hipFree(h->d_fin_tail); hipFree(h->d_chain);
+    h->d_fin_tail = nullptr; h->d_chain = nullptr;
     hipFree(h->d_fin_score); hipFree(h->d_best_lab); hipFree(h->d_best_len);
     hipFree(h->d_best_score);
     hipHostFree(h->h_best_lab); hipHostFree(h->h_best_len); hipHostFree(h->h_status);
@@ -285,7 +289,9 @@ int ensure_ws(asr_ctc* h, int B, int T) {
     hipDeviceSynchronize();
     free_ws(h);
     const size_t kc = (size_t)h->kcap;
-    ASR_HIP_TRY(hipMalloc(&h->d_nodes, sizeof(int2) * (size_t)nB * nT * kc));
+    ASR_HIP_TRY(hipMalloc(&h->d_nodes, sizeof(int4) * (size_t)nB * nT * kc));
+    ASR_HIP_TRY(hipMalloc(&h->d_fin_tail, sizeof(uint64_t) * nB * kc));
+    ASR_HIP_TRY(hipMalloc(&h->d_chain, sizeof(int) * (size_t)nB * 2 * (nT / 8 + 1)));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_n, sizeof(int) * nB));
     ASR_HIP_TRY(hipMalloc(&h->d_status, sizeof(int) * nB));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_node, sizeof(int) * nB * kc));
@@ -413,6 +419,7 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     a.nodes = h->d_nodes;
     a.fin_n = h->d_fin_n;
     a.fin_node = h->d_fin_node;
+    a.fin_tail = h->d_fin_tail;
     a.fin_score = h->d_fin_score;
     a.status = h->d_status;
     a.best_lab = h->d_best_lab;
@@ -431,7 +438,7 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     rc = asr::ctc_launch_decode(a, waves, st);
     if (rc) return rc;
     ASR_HIP_TRY(hipEventRecord(h->ev1, st));
-    rc = asr::ctc_launch_best(a, h->d_codes, st);
+    rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, st);
     if (rc) return rc;
     h->have = true;
     h->last_emis = d_emis;
