@@ -35,6 +35,7 @@ struct CtcArgs {
     uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
 };
 
+int ctc_row_capacity(int kcap);   // compile-time slot capacity KC >= kcap (64, 128, 256)
 size_t ctc_lds_bytes(const CtcGeom& g);
 int ctc_launch_decode_v8(const CtcArgs& a, int waves, int rpt, hipStream_t s);
 int ctc_launch_decode_v32(const CtcArgs& a, int waves, int rpt, hipStream_t s);

@@ -4,7 +4,15 @@
 
 namespace asr {
 
-size_t ctc_lds_bytes(const CtcGeom& g) { return lds_plan(g).total; }
+int ctc_row_capacity(int kcap) { return kcap <= 64 ? 64 : (kcap <= 128 ? 128 : 256); }
+
+size_t ctc_lds_bytes(const CtcGeom& g) {
+    switch (ctc_row_capacity(g.kcap)) {
+    case 64: return Lds<64>::total(g.ch, g.V);
+    case 128: return Lds<128>::total(g.ch, g.V);
+    default: return Lds<256>::total(g.ch, g.V);
+    }
+}
 
 // A hypothesis is (node, tail): the chain of 8-label blocks ending at node
 // (each record: parent node, 8 labels packed 8 bits each, first label lowest)
@@ -143,7 +151,7 @@ __global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, in
 
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s) {
     const int R = a.g.V + 1;
-    const int rpt = a.g.kcap <= 64 ? 1 : (a.g.kcap <= 128 ? 2 : 4);
+    const int rpt = ctc_row_capacity(a.g.kcap) / 64;   // rows per thread: the layout's KC
     if (R <= 8) return ctc_launch_decode_v8(a, waves, rpt, s);
     if (R <= 32) return ctc_launch_decode_v32(a, waves, rpt, s);
     if (R <= 64) return ctc_launch_decode_v64(a, waves, rpt, s);

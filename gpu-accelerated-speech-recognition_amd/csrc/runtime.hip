@@ -262,9 +262,7 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
     g.sb = (h->V + 1) <= 32 ? 5 : 6;
     const int nt = 64 * waves;
     g.ch = std::max(1, std::min(32, 16 * nt / h->V));
-    int ht = 64;
-    while (ht < 4 * h->kcap) ht <<= 1;
-    g.ht = ht;
+    g.ht = 4 * asr::ctc_row_capacity(h->kcap);
     return g;
 }
 
