@@ -260,8 +260,8 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
     g.K = h->K;
     g.kcap = h->kcap;
     g.sb = (h->V + 1) <= 32 ? 5 : 6;
-    const int nt = 64 * waves;
-    g.ch = std::max(1, std::min(32, 16 * nt / h->V));
+    (void)waves;
+    g.ch = std::max(1, std::min(32, 1024 / h->V));   // chunk = ch*V <= 1024 emissions (16 per thread at 1 wave)
     g.ht = 4 * asr::ctc_row_capacity(h->kcap);
     return g;
 }
