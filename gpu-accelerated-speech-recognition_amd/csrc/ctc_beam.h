@@ -8,13 +8,14 @@ constexpr int NSTAMP = 16;   // diagnostic phase clocks per utterance
 
 // Launch geometry of one decode, shared by the host planner and the kernel.
 struct CtcGeom {
-    int V;       // labels incl. blank (<= 63)
+    int V;       // labels incl. blank (<= 63: register kernels; larger: wide kernel)
     int blank;   // blank label id
     int K;       // beamWidth + 1 states kept (cpp:107 cutoff index)
     int kcap;    // slot/state capacity incl. ties at the cutoff
     int sb;      // log2 of the candidate row stride (row = V+1 columns)
     int ch;      // emission frames staged per prefetch chunk
-    int ht;      // orphan-group table cells (power of two >= 4*kcap, 8-cell buckets)
+    int ht;      // orphan-table cells (4 x row capacity, 8-cell buckets)
+    int lbits;   // bits per label in node records and tails: 8 (V <= 64) or 16
 };
 
 struct CtcArgs {
@@ -22,7 +23,8 @@ struct CtcArgs {
     const float* emis;      // [T][B][V]
     int T, B;
     int is_log;
-    uint64_t blank_less;    // bit c: code(blank) < code(c)
+    uint64_t blank_less;    // bit c: code(blank) < code(c)   (V <= 64 kernels)
+    const int* codes;       // [V] symbol codes (device; wide-vocabulary kernel)
     int4* nodes;            // [B][T*kcap] (parent node, 0, 8 labels packed lo, hi)
     int* fin_n;             // [B] final hypotheses
     int* fin_node;          // [B][kcap]
@@ -43,6 +45,10 @@ int ctc_launch_decode_v64(const CtcArgs& a, int waves, int rpt, hipStream_t s);
 int ctc_set_max_lds_v8();
 int ctc_set_max_lds_v32();
 int ctc_set_max_lds_v64();
+constexpr int WIDE_VMAX = 4096;   // largest vocabulary of the wide kernel (ctc_wide_kernel.inc)
+int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
+size_t ctc_lds_bytes_wide(int kc, int V);
+int ctc_set_max_lds_wide();
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s);
 int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);

@@ -7,6 +7,7 @@ namespace asr {
 int ctc_row_capacity(int kcap) { return kcap <= 64 ? 64 : (kcap <= 128 ? 128 : 256); }
 
 size_t ctc_lds_bytes(const CtcGeom& g) {
+    if (g.V + 1 > 64) return ctc_lds_bytes_wide(ctc_row_capacity(g.kcap), g.V);
     switch (ctc_row_capacity(g.kcap)) {
     case 64: return Lds<64>::total(g.ch, g.V);
     case 128: return Lds<128>::total(g.ch, g.V);
@@ -19,9 +20,14 @@ size_t ctc_lds_bytes(const CtcGeom& g) {
 // followed by the tail's labels.  Links always point to earlier frames, so a
 // chain has at most T/8 blocks; the bounds only guard a corrupted table.
 
-__device__ __forceinline__ uint32_t block_label(const int4 r, int k) {
+// Labels are lbits wide: 8 (8 per record, up to 7 in a tail) or 16 (4 per
+// record, up to 3 in a tail, wide-vocabulary kernel).
+__device__ __forceinline__ uint32_t block_label(const int4 r, int k, int lbits) {
     const uint64_t pk = ((uint64_t)(uint32_t)r.w << 32) | (uint32_t)r.z;
-    return (uint32_t)(pk >> (8 * k)) & 0xFFu;
+    return (uint32_t)(pk >> (lbits * k)) & ((1u << lbits) - 1u);
+}
+__device__ __forceinline__ uint32_t tail_label(uint64_t tail, int k, int lbits) {
+    return (uint32_t)(tail >> (lbits * k)) & ((1u << lbits) - 1u);
 }
 
 // Chase the block chain of `x` into ids[] (last block first); returns the
@@ -34,14 +40,16 @@ __device__ int chase_blocks(const int4* nodes, int nmax, int x, int* ids, int ma
 
 // Label k (from the front) of a hypothesis whose blocks are ids[0..nb)
 // (last first) followed by tail.
-__device__ uint32_t label_at(const int4* nodes, const int* ids, int nb, uint64_t tail, int k) {
-    if (k < 8 * nb) return block_label(nodes[ids[nb - 1 - k / 8]], k % 8);
-    return (uint32_t)(tail >> (8 * (k - 8 * nb))) & 0xFFu;
+__device__ uint32_t label_at(const int4* nodes, const int* ids, int nb, uint64_t tail, int k,
+                             int lbits) {
+    const int per = 64 / lbits;
+    if (k < per * nb) return block_label(nodes[ids[nb - 1 - k / per]], k % per, lbits);
+    return tail_label(tail, k - per * nb, lbits);
 }
 
 // Best-path traceback: per utterance, the maximum final score; among ties the
 // smallest code string (std::map order, cpp:76-84).  Labels are written in
-// forward order to best_lab[b][T].  chain: [B][2][T/8+1] scratch.
+// forward order to best_lab[b][T].  chain: [B][2][T/4+1] scratch.
 __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* codes, int* chain) {
     const int b = blockIdx.x, lane = threadIdx.x;
     const int kcap = a.g.kcap;
@@ -51,7 +59,8 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
     const uint64_t* ft = a.fin_tail + (size_t)b * kcap;
     const int4* nodes = a.nodes + (size_t)b * a.T * kcap;
     const int nmax = a.T * kcap;
-    const int maxb = a.T / 8 + 1;
+    const int lbits = a.g.lbits, per = 64 / lbits;
+    const int maxb = a.T / 4 + 1;
     int* ids = chain + (size_t)b * 2 * maxb;   // best candidate's blocks
     int* ids2 = ids + maxb;                    // challenger's (ties only)
     int* out = a.best_lab + (size_t)b * a.T;
@@ -74,12 +83,12 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
                 continue;
             }
             const int nb2 = chase_blocks(nodes, nmax, fn[i], ids2, maxb);
-            const int li = 8 * nb2 + (int)(ft[i] >> 56), lb = 8 * nb + (int)(ft[bi] >> 56);
+            const int li = per * nb2 + (int)(ft[i] >> 56), lb = per * nb + (int)(ft[bi] >> 56);
             const int lmin = li < lb ? li : lb;
             bool less = li < lb, decided = false;
             for (int k = 0; k < lmin && !decided; k++) {
-                const uint32_t yi = label_at(nodes, ids2, nb2, ft[i], k);
-                const uint32_t yb = label_at(nodes, ids, nb, ft[bi], k);
+                const uint32_t yi = label_at(nodes, ids2, nb2, ft[i], k, lbits);
+                const uint32_t yb = label_at(nodes, ids, nb, ft[bi], k, lbits);
                 const int ci = yi < (unsigned)a.g.V ? codes[yi] : 0;
                 const int cb = yb < (unsigned)a.g.V ? codes[yb] : 0;
                 if (ci != cb) { less = ci < cb; decided = true; }
@@ -103,15 +112,14 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
         return;
     }
     const uint64_t tail = ft[bi];
-    const int nt = (int)(tail >> 56) < 8 ? (int)(tail >> 56) : 7;
-    const int len = 8 * nb + nt <= a.T ? 8 * nb + nt : a.T;
+    const int nt = (int)(tail >> 56) < per ? (int)(tail >> 56) : per - 1;
+    const int len = per * nb + nt <= a.T ? per * nb + nt : a.T;
     for (int j = lane; j < nb; j += 64) {   // block j from the front
         const int4 r = nodes[ids[nb - 1 - j]];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (8 * j + k < len) out[8 * j + k] = (int)block_label(r, k);
+        for (int k = 0; k < per; k++)
+            if (per * j + k < len) out[per * j + k] = (int)block_label(r, k, lbits);
     }
-    if (lane < nt && 8 * nb + lane < len) out[8 * nb + lane] = (int)((tail >> (8 * lane)) & 0xFFu);
+    if (lane < nt && per * nb + lane < len) out[per * nb + lane] = (int)tail_label(tail, lane, lbits);
     if (lane == 0) {
         a.best_len[b] = len;
         a.best_score[b] = sc[bi];
@@ -129,22 +137,23 @@ __global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, in
     const uint64_t* ft = a.fin_tail + (size_t)b * kcap;
     const int4* nodes = a.nodes + (size_t)b * a.T * kcap;
     const int nmax = a.T * kcap;
-    const int maxb = a.T / 8 + 1;
+    const int lbits = a.g.lbits, per = 64 / lbits;
+    const int maxb = a.T / 4 + 1;
     for (int i = threadIdx.x; i < n; i += 64) {
         int* out = all_lab + ((size_t)b * kcap + i) * a.T;
         int nb = 0;
         for (int x = fn[i]; x >= 0 && x < nmax && nb < maxb; x = nodes[x].x) nb++;
         const uint64_t tail = ft[i];
-        const int nt = (int)(tail >> 56) < 8 ? (int)(tail >> 56) : 7;
-        const int len = 8 * nb + nt <= a.T ? 8 * nb + nt : a.T;
+        const int nt = (int)(tail >> 56) < per ? (int)(tail >> 56) : per - 1;
+        const int len = per * nb + nt <= a.T ? per * nb + nt : a.T;
         int j = nb - 1;
         for (int x = fn[i]; x >= 0 && x < nmax && j >= 0; x = nodes[x].x, j--) {
             const int4 r = nodes[x];
-            for (int k = 0; k < 8; k++)
-                if (8 * j + k < len) out[8 * j + k] = (int)block_label(r, k);
+            for (int k = 0; k < per; k++)
+                if (per * j + k < len) out[per * j + k] = (int)block_label(r, k, lbits);
         }
         for (int k = 0; k < nt; k++)
-            if (8 * nb + k < len) out[8 * nb + k] = (int)((tail >> (8 * k)) & 0xFFu);
+            if (per * nb + k < len) out[per * nb + k] = (int)tail_label(tail, k, lbits);
         all_len[(size_t)b * kcap + i] = len;
     }
 }
@@ -155,7 +164,7 @@ int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s) {
     if (R <= 8) return ctc_launch_decode_v8(a, waves, rpt, s);
     if (R <= 32) return ctc_launch_decode_v32(a, waves, rpt, s);
     if (R <= 64) return ctc_launch_decode_v64(a, waves, rpt, s);
-    return ASR_ERR_UNSUPPORTED;
+    return ctc_launch_decode_wide(a, rpt, s);
 }
 
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s) {
@@ -174,6 +183,7 @@ int ctc_set_max_lds() {
     int rc = ctc_set_max_lds_v8();
     if (!rc) rc = ctc_set_max_lds_v32();
     if (!rc) rc = ctc_set_max_lds_v64();
+    if (!rc) rc = ctc_set_max_lds_wide();
     return rc;
 }
 

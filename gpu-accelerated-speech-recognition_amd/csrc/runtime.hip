@@ -215,7 +215,7 @@ struct asr_ctc {
     int4* d_nodes = nullptr;
     int *d_fin_n = nullptr, *d_fin_node = nullptr, *d_status = nullptr;
     uint64_t* d_fin_tail = nullptr;
-    int* d_chain = nullptr;         // traceback scratch [B][2][T/8+1]
+    int* d_chain = nullptr;         // traceback scratch [B][2][T/4+1]
     double* d_fin_score = nullptr;
     int *d_best_lab = nullptr, *d_best_len = nullptr;
     double* d_best_score = nullptr;
@@ -260,6 +260,7 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
     g.K = h->K;
     g.kcap = h->kcap;
     g.sb = (h->V + 1) <= 32 ? 5 : 6;
+    g.lbits = (h->V + 1) <= 64 ? 8 : 16;   // labels in node records: 8 x 8 bits or 4 x 16 bits
     (void)waves;
     g.ch = std::max(1, std::min(32, 1024 / h->V));   // chunk = ch*V <= 1024 emissions (16 per thread at 1 wave)
     g.ht = 4 * asr::ctc_row_capacity(h->kcap);
@@ -289,7 +290,7 @@ int ensure_ws(asr_ctc* h, int B, int T) {
     const size_t kc = (size_t)h->kcap;
     ASR_HIP_TRY(hipMalloc(&h->d_nodes, sizeof(int4) * (size_t)nB * nT * kc));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_tail, sizeof(uint64_t) * nB * kc));
-    ASR_HIP_TRY(hipMalloc(&h->d_chain, sizeof(int) * (size_t)nB * 2 * (nT / 8 + 1)));
+    ASR_HIP_TRY(hipMalloc(&h->d_chain, sizeof(int) * (size_t)nB * 2 * (nT / 4 + 1)));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_n, sizeof(int) * nB));
     ASR_HIP_TRY(hipMalloc(&h->d_status, sizeof(int) * nB));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_node, sizeof(int) * nB * kc));
@@ -334,7 +335,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     if (!out) return ASR_ERR_ARG;
     *out = nullptr;
     if (V < 2 || beam_width < 1 || blank_id < 0 || blank_id >= V) return ASR_ERR_ARG;
-    if (V > 63) return ASR_ERR_UNSUPPORTED;
+    if (V > asr::WIDE_VMAX) return ASR_ERR_UNSUPPORTED;
     asr_ctc* h = new asr_ctc();
     h->V = V;
     h->beam = beam_width;
@@ -347,7 +348,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
             if (h->codes[u] == h->codes[v]) { delete h; return ASR_ERR_ARG; }
     h->blank_less = 0;
     for (int v = 0; v < V; v++)
-        if (h->codes[blank_id] < h->codes[v]) h->blank_less |= 1ull << v;
+        if (v < 64 && h->codes[blank_id] < h->codes[v]) h->blank_less |= 1ull << v;
     // Automatic capacity: K plus room for ties at the cutoff; an overflow is
     // detected on the device and the decode is re-run with more room.
     h->auto_cap = max_states <= 0;
@@ -414,6 +415,7 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     a.B = B;
     a.is_log = is_log ? 1 : 0;
     a.blank_less = h->blank_less;
+    a.codes = h->d_codes;
     a.nodes = h->d_nodes;
     a.fin_n = h->d_fin_n;
     a.fin_node = h->d_fin_node;

@@ -58,11 +58,14 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--waves", default="1,2,4")
+    ap.add_argument("--cases", default="c2,c3")
     args = ap.parse_args()
     global WAVES
     WAVES = [int(x) for x in args.waves.split(",")]
     asr.set_device(0)
-    ap_cases = [(500, 64, 29, 50), (1000, 256, 29, 100)]
+    ap_cases = {"c2": (500, 64, 29, 50), "c3": (1000, 256, 29, 100),
+                "c5": (2000, 32, 1000, 200)}   # C5: 32 utterances per GPU
+    ap_cases = [ap_cases[c] for c in args.cases.split(",")]
     for (T, B, V, beam) in ap_cases:
         for sigma in (3.0, 0.5):
             for waves in WAVES:
