@@ -91,3 +91,23 @@ def test_wide_long_utterance_best():
         assert best[b] == ref[b][0][0]
         assert abs(lp[b] - ref[b][0][1]) <= 1e-9 * abs(ref[b][0][1])
     dec.close()
+
+
+def test_wide_blank_dominant_frames():
+    """The blank often carries the largest emission (as in trained CTC
+    models): the selection's key bound must include it."""
+    T, B, V, beam = 40, 2, 300, 100
+    emis = oracle.synthetic_emissions(T, B, V, seed0=15).astype(np.float64)
+    emis[::2, :, 0] *= 50.0                 # every other frame: blank dominant
+    emis /= emis.sum(axis=2, keepdims=True)
+    emis = emis.astype(np.float32)
+    ref = oracle.decode(emis, beam, 0, nthreads=cpu_threads())
+    assert_beams_equal(gpu_beams(emis, beam), ref, "blank dominant")
+
+
+def test_wide_c5_longer():
+    """BASELINE C5 vocabulary and beam over 40 frames (best path and score)."""
+    T, B, V, beam = 40, 1, 1000, 200
+    emis = oracle.synthetic_emissions(T, B, V, seed0=16)
+    ref = oracle.decode(emis, beam, 0, nthreads=cpu_threads(), max_hyps=beam + 1)
+    assert_beams_equal([x[:beam + 1] for x in gpu_beams(emis, beam)], ref, "C5 T=40")
