@@ -8,7 +8,7 @@ enum GemmEpilogue {
     EPI_NONE = 0,        // C = A.B
     EPI_BIAS = 1,        // C = A.B + b1
     EPI_BIAS_RELU = 2,   // C = max(A.B + b1, 0)
-    EPI_LOGSOFTMAX = 3,  // C = log_softmax(A.B + b1) per row, N <= 64
+    EPI_LOGSOFTMAX = 3,  // C = log_softmax(A.B + b1) per row (fused for N <= 64)
     EPI_DUAL_TANH = 4,   // C = tanh((A.B + A2.B2) + (b2 + b1))
     EPI_ADD_TANH = 5     // C = tanh((D + A.B) + (b2 + b1)); C may alias D
 };
@@ -31,5 +31,6 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
                      float* hid, int T, int B, int H, hipStream_t s);
 int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
 int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
+int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);
 
 }  // namespace asr

@@ -183,7 +183,13 @@ static int launch_gemm_epi(const GemmArgs& g, hipStream_t s) {
 
 int gemm_launch(const GemmArgs& g, int epi, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return ASR_ERR_ARG;
-    if (epi == EPI_LOGSOFTMAX && g.N > 64) return ASR_ERR_UNSUPPORTED;
+    if (epi == EPI_LOGSOFTMAX && g.N > 64) {
+        // Rows wider than one workgroup tile (e.g. C5's V = 1000): bias GEMM,
+        // then a row-wise log_softmax pass in place (model.py:49).
+        const int rc = gemm_launch(g, EPI_BIAS, s);
+        if (rc) return rc;
+        return row_logsoftmax_launch(g.C, g.ldc, g.M, g.N, s);
+    }
     switch (epi) {
         case EPI_NONE: return launch_gemm_epi<EPI_NONE>(g, s);
         case EPI_BIAS: return launch_gemm_epi<EPI_BIAS>(g, s);
@@ -267,6 +273,32 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
     if (H > RNN_HMAX) return ASR_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(rnn_recur_kernel, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid,
                        T, B, H);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// In-place log_softmax of each row of C[M][ldc] (first N columns): one wave
+// per row, max and sum of exp by shuffle reductions.
+__global__ __launch_bounds__(256) void row_logsoftmax_kernel(float* __restrict__ C, long ldc, int M,
+                                                             int N) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= M) return;
+    float* r = C + (long)row * ldc;
+    float mx = -INFINITY;
+    for (int c = lane; c < N; c += 64) mx = fmaxf(mx, r[c]);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+    for (int c = lane; c < N; c += 64) sum += expf(r[c] - mx);
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float lz = mx + logf(sum);
+    for (int c = lane; c < N; c += 64) r[c] -= lz;
+}
+
+int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s) {
+    if (M <= 0) return ASR_OK;
+    hipLaunchKernelGGL(row_logsoftmax_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, C, ldc,
+                       M, N);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

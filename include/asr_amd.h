@@ -93,7 +93,8 @@ typedef enum asr_epilogue {
 } asr_epilogue;
 
 /* Linear::forward (Linear.cu:42-49): y[M,N] = epi(x[M,K] . W[K,N] + b[N]).
- * ASR_EPI_BIAS_LOGSOFTMAX needs N <= 64. */
+ * ASR_EPI_BIAS_LOGSOFTMAX is fused into the GEMM for N <= 64 and a row pass
+ * after it otherwise. */
 int asr_linear_fwd(const float* d_x, const float* d_W, const float* d_b, float* d_y, int M,
                    int K, int N, int epilogue, asr_stream_t s);
 

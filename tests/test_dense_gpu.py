@@ -86,7 +86,7 @@ def test_linear_random(M, K, N, epi):
     close(y.toCpu(), ref.numpy())
 
 
-@pytest.mark.parametrize("M,K,N", [(32000, 256, 29), (100, 64, 5), (77, 30, 64)])
+@pytest.mark.parametrize("M,K,N", [(32000, 256, 29), (100, 64, 5), (77, 30, 64), (300, 1024, 1000), (9, 16, 65)])
 def test_linear_logsoftmax(M, K, N):
     rng = np.random.default_rng(N)
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
@@ -166,3 +166,44 @@ def test_rnn_cell_forward():
     ref = torch.tanh((torch.from_numpy(x) @ torch.from_numpy(w_ih) + torch.from_numpy(h) @ torch.from_numpy(w_hh))
                      + (torch.from_numpy(b_hh) + torch.from_numpy(b_ih)))
     close(out.toCpu(), ref.numpy(), 5e-5)
+
+
+def test_rnn_forward_c5_hidden():
+    """BASELINE C5 hidden size (H = in = 1024): the per-step fused-cell path."""
+    T, B, I, H = 6, 4, 1024, 1024
+    rng = np.random.default_rng(1024)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    hid = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dm(x), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B)
+    close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 1e-4)
+
+
+def test_rnn_multilayer():
+    """num_layers > 1 (RNN.h:13-20): layer l+1 consumes layer l's hiddens."""
+    T, B, I, H, L = 15, 6, 40, 64, 3
+    rng = np.random.default_rng(77)
+    s = 1 / np.sqrt(H)
+    params = []
+    for l in range(L):
+        i = I if l == 0 else H
+        params.append((rng.uniform(-s, s, (i, H)).astype(np.float32),
+                       rng.uniform(-s, s, (H, H)).astype(np.float32),
+                       rng.uniform(-0.1, 0.1, H).astype(np.float32),
+                       rng.uniform(-0.1, 0.1, H).astype(np.float32)))
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    rnn = asr.RNN(B, I, H, T, L, params)
+    out = rnn.forward(dm(x)).toCpu()
+    ref = torch.nn.RNN(I, H, L)
+    with torch.no_grad():
+        for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(params):
+            getattr(ref, f"weight_ih_l{l}").copy_(torch.from_numpy(w_ih.T))
+            getattr(ref, f"weight_hh_l{l}").copy_(torch.from_numpy(w_hh.T))
+            getattr(ref, f"bias_ih_l{l}").copy_(torch.from_numpy(b_ih))
+            getattr(ref, f"bias_hh_l{l}").copy_(torch.from_numpy(b_hh))
+        y, _ = ref(torch.from_numpy(x.reshape(T, B, I)))
+    close(out, y.reshape(T * B, H).numpy(), 5e-5)
