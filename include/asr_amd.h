@@ -120,10 +120,12 @@ typedef struct asr_ctc asr_ctc_t;
 
 /* Constructor CTCBeamSearch(char* vocab, int vocabSize, int beamWidth, int blankID)
  * (h:107).  codes[V] is the symbol code of each label (the vocab char as
- * unsigned char for the reference API; NULL = label id).  Hypothesis order on
+ * unsigned char for the reference API; NULL = label id, the label-id
+ * overload SURVEY a2 asks for large vocabularies).  Hypothesis order on
  * ties is code-string order, as std::string order in the reference.
- * max_states bounds the beam incl. ties at the cutoff (0 = automatic,
- * >= beamWidth+1). */
+ * V up to 4096 (V > 63 runs the large-vocabulary kernel, e.g. C5 V=1000);
+ * beam_width + 1 + ties <= 256.  max_states bounds the beam incl. ties at the
+ * cutoff (0 = automatic, >= beamWidth+1). */
 int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, int max_states,
                    asr_ctc_t** out);
 int asr_ctc_destroy(asr_ctc_t* h);
