@@ -278,6 +278,82 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 }
 
 // ---------------------------------------------------------------------------
+// One recurrence step for H > 256 (W_hh too large to stay on one CU):
+// h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)) in place over P_t
+// (RNN_Cell.cu:10-12 order).  Small M (the batch) and wide N: each
+// workgroup owns 8 output columns for 32 batch rows; its W_hh column slice
+// [H][8] is staged in LDS once, h_{t-1} rows are read as float4 (the 8
+// threads of a row read the same addresses).  Grid (H/8, ceil(B/32)).
+constexpr int RS_COLS = 8;
+constexpr int RS_KS = 4;   // K split: 4 x 256 threads, partial sums combined in LDS
+
+__global__ __launch_bounds__(256 * RS_KS) void rnn_step_kernel(float* __restrict__ ht,
+                                                               const float* __restrict__ hp,
+                                                               const float* __restrict__ Whh,
+                                                               const float* __restrict__ b_ih,
+                                                               const float* __restrict__ b_hh, int B,
+                                                               int H) {
+    // ws[c][k]: the workgroup's W_hh columns, column-major with a padded
+    // stride (float4 reads; the 8 columns of a wave hit distinct banks),
+    // staged with float4 loads.  h_{t-1} rows stream from L2 as float4; the
+    // K range is split over 4 thread groups so that each dependent-latency
+    // chain is a quarter as long, 16 loads in flight per thread.
+    extern __shared__ float ws[];
+    const int ld = H + 4;
+    float* part = ws + RS_COLS * ld;   // [RS_KS][256] partial sums
+    const int n0 = blockIdx.x * RS_COLS, r0 = blockIdx.y * 32;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < H * (RS_COLS / 4); i += 256 * RS_KS) {   // H % 8 == 0
+        const int k = i / (RS_COLS / 4), c4 = (i - k * (RS_COLS / 4)) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(Whh + (long)k * H + n0 + c4);
+        ws[(c4 + 0) * ld + k] = v.x;
+        ws[(c4 + 1) * ld + k] = v.y;
+        ws[(c4 + 2) * ld + k] = v.z;
+        ws[(c4 + 3) * ld + k] = v.w;
+    }
+    __syncthreads();
+    const int ks = tid / 256, o = tid % 256;
+    const int r = r0 + o / RS_COLS, c = o % RS_COLS, n = n0 + c;
+    const int q4 = H / 4, kb = ks * q4 / RS_KS, ke = (ks + 1) * q4 / RS_KS;
+    float acc = 0.f;
+    if (r < B) {
+        const float4* h4 = reinterpret_cast<const float4*>(hp + (long)r * H);
+        const float4* w4 = reinterpret_cast<const float4*>(ws + c * ld);
+#pragma unroll 16
+        for (int k4 = kb; k4 < ke; k4++) {
+            const float4 v = h4[k4], w = w4[k4];
+            acc = fmaf(v.x, w.x, acc);
+            acc = fmaf(v.y, w.y, acc);
+            acc = fmaf(v.z, w.z, acc);
+            acc = fmaf(v.w, w.w, acc);
+        }
+    }
+    part[ks * 256 + o] = acc;
+    __syncthreads();
+    if (ks != 0 || r >= B) return;
+    const float hh = ((part[o] + part[256 + o]) + part[512 + o]) + part[768 + o];
+    float* out = ht + (long)r * H + n;
+    *out = tanhf((*out + hh) + (b_hh[n] + b_ih[n]));
+}
+
+int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
+                    const float* b_hh, int B, int H, hipStream_t s) {
+    const size_t lds = sizeof(float) * ((size_t)(H + 4) * RS_COLS + 256 * RS_KS);
+    if ((H % RS_COLS) != 0) return ASR_ERR_UNSUPPORTED;   // float4 column slices
+    if (lds > 160 * 1024) return ASR_ERR_UNSUPPORTED;
+    static bool attr = false;
+    if (!attr) {
+        ASR_HIP_TRY(hipFuncSetAttribute((const void*)rnn_step_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    const dim3 grid((unsigned)((H + RS_COLS - 1) / RS_COLS), (unsigned)((B + 31) / 32));
+    hipLaunchKernelGGL(rnn_step_kernel, grid, dim3(256 * RS_KS), lds, s, ht, hp, Whh, b_ih, b_hh, B, H);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // In-place log_softmax of each row of C[M][ldc] (first N columns): one wave
 // per row, max and sum of exp by shuffle reductions.
 __global__ __launch_bounds__(256) void row_logsoftmax_kernel(float* __restrict__ C, long ldc, int M,

@@ -186,13 +186,16 @@ int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float*
     if (rc) return rc;
     // 2. recurrence, in place over hid.
     if (H <= 256) return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
-    // H > 256: one fused cell GEMM per step, h_t = tanh((P_t + h_{t-1}.W_hh) + bias).
+    // H > 256: one small-M step kernel per frame (W_hh slice per workgroup in
+    // LDS), h_t = tanh((P_t + h_{t-1}.W_hh) + bias) in place.
     for (int t = 0; t < T; t++) {
         float* ht = hid + (size_t)t * B * H;
         const float* hp = t == 0 ? h0 : hid + (size_t)(t - 1) * B * H;
         if (!hp) {   // h_{-1} = 0 (RNN.h:15-16 zero-filled h_0s)
             rc = asr::bias_tanh_launch(ht, b_ih, b_hh, (long)B * H, H, st);
-        } else {
+        } else if ((H & 7) == 0) {
+            rc = asr::rnn_step_launch(ht, hp, W_hh, b_ih, b_hh, B, H, st);
+        } else {   // odd widths: the fused cell GEMM
             asr::GemmArgs g = gemm_args(hp, W_hh, ht, B, H, H);
             g.D = ht; g.b1 = b_ih; g.b2 = b_hh;
             rc = asr::gemm_launch(g, asr::EPI_ADD_TANH, st);

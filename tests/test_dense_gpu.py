@@ -134,7 +134,7 @@ def _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0=None):
 
 
 @pytest.mark.parametrize("T,B,I,H", [(50, 64, 256, 256), (20, 3, 10, 50), (9, 5, 40, 128),
-                                     (12, 4, 24, 300), (6, 2, 8, 1)])
+                                     (12, 4, 24, 300), (6, 2, 8, 1), (7, 40, 16, 258)])
 def test_rnn_forward(T, B, I, H):
     rng = np.random.default_rng(H)
     x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
