@@ -48,7 +48,7 @@ EXPORTS = [
     "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
     "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
-    "asr_ctc_get_config",
+    "asr_ctc_get_config", "asr_ctc_decode_ex",
 ]
 
 
@@ -108,6 +108,7 @@ def lib() -> ctypes.CDLL:
         "asr_ctc_last_kernel_ms": [_vp, ctypes.POINTER(_f)],
         "asr_ctc_set_waves": [_vp, _i],
         "asr_ctc_get_config": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
+        "asr_ctc_decode_ex": [_vp, _vp, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -303,19 +304,37 @@ class CTCDecoder:
     def set_waves(self, waves: int) -> None:
         check(lib().asr_ctc_set_waves(self.h, waves), "asr_ctc_set_waves")
 
-    def decode_device(self, d_emis: int, T: int, B: int, is_log: bool, stream: int = 0) -> None:
-        check(lib().asr_ctc_decode(self.h, d_emis, T, B, int(bool(is_log)), stream), "asr_ctc_decode")
+    def decode_device(self, d_emis: int, T: int, B: int, is_log: bool, stream: int = 0,
+                      lengths: Optional[Sequence[int]] = None, frame_stride: Optional[int] = None,
+                      utt_stride: Optional[int] = None) -> None:
+        """Decode device emissions: element (t, b, v) at d_emis[t*frame_stride +
+        b*utt_stride + v] (default time-major [T][B][V]); lengths[b] <= T."""
+        fs = B * self.V if frame_stride is None else int(frame_stride)
+        us = self.V if utt_stride is None else int(utt_stride)
+        ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.int32)
+        if ln is not None:
+            assert ln.shape == (B,), (ln.shape, B)
+        check(lib().asr_ctc_decode_ex(self.h, d_emis, T, B, fs, us,
+                                      _ptr(ln) if ln is not None else None, int(bool(is_log)), stream),
+              "asr_ctc_decode_ex")
         self.T, self.B = T, B
 
-    def decode(self, emis: np.ndarray, is_log: bool = False, stream: int = 0) -> None:
-        """Upload emis [T][B][V] (fp32) and enqueue the decode."""
+    def decode(self, emis: np.ndarray, is_log: bool = False, stream: int = 0,
+               lengths: Optional[Sequence[int]] = None, batch_major: bool = False) -> None:
+        """Upload emissions (fp32 [T][B][V], or [B][T][V] with batch_major) and
+        enqueue the decode; lengths[b] frames of utterance b are used."""
         emis = np.ascontiguousarray(emis, dtype=np.float32)
-        T, B, V = emis.shape
+        if batch_major:
+            B, T, V = emis.shape
+            fs, us = V, T * V
+        else:
+            T, B, V = emis.shape
+            fs, us = B * V, V
         assert V == self.V, (V, self.V)
         if self._emis is None or self._emis.nbytes < emis.nbytes:
             self._emis = DeviceBytes(emis.nbytes)
         check(lib().asr_memcpy_h2d(self._emis.ptr, _ptr(emis), emis.nbytes, stream), "asr_memcpy_h2d")
-        self.decode_device(self._emis.ptr, T, B, is_log, stream)
+        self.decode_device(self._emis.ptr, T, B, is_log, stream, lengths, fs, us)
 
     def best_arrays(self, allow_overflow: bool = False) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Best hypotheses as arrays: labels [B][T] int32 (row b valid up to
@@ -389,3 +408,53 @@ class CTCBeamSearch:
         labels, lp = self._dec.best()
         self.logprobs = lp
         return [("".join(self.vocab[i] for i in lab), float(np.exp(l))) for lab, l in zip(labels, lp)]
+
+
+class CTCBeamDecoder:
+    """Batch interface of the Python baseline's decoder (baseline/main.py:10,
+    29, 46: ctcdecode.CTCBeamDecoder(labels, beam_width=, blank_id=,
+    num_processes=, log_probs_input=True).decode(probs[B,T,V], seq_lens)) on
+    this library's decoder.  ctcdecode itself is not available here, so the
+    search semantics are the reference C++ decoder's (CTCBeamSearch.cpp with
+    F1-F3), not ctcdecode's; no language model (model_path must
+    be None).  decode returns (beam_results [B, beam_width, T] int32 label
+    ids, beam_scores [B, beam_width] float32 = -log p (lower is better),
+    timesteps [B, beam_width, T] int32 = -1 (not tracked), out_lens
+    [B, beam_width] int32); hypotheses beyond an utterance's final beam have
+    length 0 and score +inf.  probs may be a numpy array or a torch tensor
+    (a GPU tensor is decoded in place, no copy)."""
+
+    def __init__(self, labels: Sequence[str], model_path: Optional[str] = None, alpha: float = 0.0,
+                 beta: float = 0.0, cutoff_top_n: int = 40, cutoff_prob: float = 1.0,
+                 beam_width: int = 100, num_processes: int = 4, blank_id: int = 0,
+                 log_probs_input: bool = False):
+        if model_path is not None:
+            raise NotImplementedError("language-model scoring is not supported")
+        self.labels = list(labels)
+        self.beam_width, self.blank_id, self.log_probs_input = beam_width, blank_id, log_probs_input
+        self._dec = CTCDecoder(len(self.labels), beam_width, blank_id)
+
+    def decode(self, probs, seq_lens=None):
+        B, T, V = (int(x) for x in probs.shape)
+        lens = None if seq_lens is None else np.asarray(
+            seq_lens.cpu().numpy() if hasattr(seq_lens, "cpu") else seq_lens, dtype=np.int32)
+        if hasattr(probs, "is_cuda") and probs.is_cuda:   # torch GPU tensor: zero-copy
+            import torch
+            p = probs if probs.dtype == torch.float32 else probs.float()
+            self._dec.decode_device(p.data_ptr(), T, B, self.log_probs_input,
+                                    torch.cuda.current_stream().cuda_stream, lens,
+                                    p.stride(1), p.stride(0))
+        else:
+            arr = probs.cpu().numpy() if hasattr(probs, "cpu") else np.asarray(probs)
+            self._dec.decode(arr, is_log=self.log_probs_input, lengths=lens, batch_major=True)
+        K = self.beam_width
+        beams = self._dec.beams(max_hyps=self._dec.config()[0])
+        results = np.zeros((B, K, T), np.int32)
+        scores = np.full((B, K), np.inf, np.float32)
+        out_lens = np.zeros((B, K), np.int32)
+        for b, hyps in enumerate(beams):
+            for k, (lab, lp) in enumerate(hyps[:K]):
+                results[b, k, :len(lab)] = lab
+                scores[b, k] = -lp
+                out_lens[b, k] = len(lab)
+        return results, scores, np.full((B, K, T), -1, np.int32), out_lens

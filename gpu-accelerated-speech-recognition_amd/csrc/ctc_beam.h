@@ -20,7 +20,9 @@ struct CtcGeom {
 
 struct CtcArgs {
     CtcGeom g;
-    const float* emis;      // [T][B][V]
+    const float* emis;      // element (t, b, v) at emis[t*tstride + b*ustride + v]
+    long tstride, ustride;  // time-major [T][B][V]: B*V, V; batch-major [B][T][V]: V, T*V
+    const int* lengths;     // [B] frames per utterance (device; NULL = T for all)
     int T, B;
     int is_log;
     uint64_t blank_less;    // bit c: code(blank) < code(c)   (V <= 64 kernels)

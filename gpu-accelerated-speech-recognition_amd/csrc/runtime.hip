@@ -239,7 +239,12 @@ struct asr_ctc {
     bool auto_cap = true;           // max_states chosen by the library
     asr_ctc* wide = nullptr;        // re-decode handle for tie overflow
     const float* last_emis = nullptr;
+    long last_tstride = 0, last_ustride = 0;
+    std::vector<int32_t> last_lengths;   // empty = all T
     int last_is_log = 0;
+    int* d_lengths = nullptr;        // per-utterance frames (asr_ctc_decode_ex)
+    int* h_lengths = nullptr;        // pinned staging
+    int cap_len = 0;
 };
 
 namespace {
@@ -381,6 +386,8 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     hipDeviceSynchronize();
     free_ws(h);
     hipFree(h->d_codes);
+    hipFree(h->d_lengths);
+    hipHostFree(h->h_lengths);
     hipFree(h->d_all_lab);
     hipFree(h->d_all_len);
     hipFree(h->d_stamps);
@@ -407,13 +414,40 @@ int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes
 }
 
 int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, asr_stream_t s) {
-    if (!h || !d_emis || T < 1 || B < 1) return ASR_ERR_ARG;
+    if (!h) return ASR_ERR_ARG;
+    return asr_ctc_decode_ex(h, d_emis, T, B, (long)B * h->V, h->V, nullptr, is_log, s);
+}
+
+int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long frame_stride,
+                      long utt_stride, const int32_t* h_lengths, int is_log, asr_stream_t s) {
+    if (!h || !d_emis || T < 1 || B < 1 || frame_stride < 1 || utt_stride < 1) return ASR_ERR_ARG;
+    if (h_lengths)
+        for (int b = 0; b < B; b++)
+            if (h_lengths[b] < 0 || h_lengths[b] > T) return ASR_ERR_ARG;
     int rc = ensure_ws(h, B, T);
     if (rc) return rc;
+    const hipStream_t st0 = asr_stream(s);
+    if (h_lengths) {   // stage the lengths through pinned memory (stream-ordered)
+        if (h->cap_len < B) {
+            hipStreamSynchronize(st0);
+            hipFree(h->d_lengths);
+            hipHostFree(h->h_lengths);
+            h->d_lengths = nullptr; h->h_lengths = nullptr; h->cap_len = 0;
+            ASR_HIP_TRY(hipMalloc(&h->d_lengths, sizeof(int) * B));
+            ASR_HIP_TRY(hipHostMalloc((void**)&h->h_lengths, sizeof(int) * B, 0));
+            h->cap_len = B;
+        }
+        ASR_HIP_TRY(hipStreamSynchronize(st0));   // the pinned copy may still be in flight
+        std::memcpy(h->h_lengths, h_lengths, sizeof(int) * B);
+        ASR_HIP_TRY(hipMemcpyAsync(h->d_lengths, h->h_lengths, sizeof(int) * B, hipMemcpyHostToDevice, st0));
+    }
     const int waves = valid_waves(h, h->waves_override ? h->waves_override : auto_waves(h->K));
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
+    a.tstride = frame_stride;
+    a.ustride = utt_stride;
+    a.lengths = h_lengths ? h->d_lengths : nullptr;
     a.T = T;
     a.B = B;
     a.is_log = is_log ? 1 : 0;
@@ -445,6 +479,9 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     if (rc) return rc;
     h->have = true;
     h->last_emis = d_emis;
+    h->last_tstride = frame_stride;
+    h->last_ustride = utt_stride;
+    h->last_lengths.assign(h_lengths ? h_lengths : nullptr, h_lengths ? h_lengths + B : nullptr);
     h->last_is_log = is_log ? 1 : 0;
     h->lastT = T;
     h->lastB = B;
@@ -475,7 +512,9 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
             if (rc) return rc;
             h->wide->auto_cap = true;
         }
-        int rc = asr_ctc_decode(h->wide, h->last_emis, T, B, h->last_is_log, h->stream);
+        int rc = asr_ctc_decode_ex(h->wide, h->last_emis, T, B, h->last_tstride, h->last_ustride,
+                                   h->last_lengths.empty() ? nullptr : h->last_lengths.data(),
+                                   h->last_is_log, h->stream);
         if (rc) return rc;
         return asr_ctc_get_best(h->wide, labels, max_len, lengths, logp);
     }
@@ -527,7 +566,9 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
             if (rc) return rc;
             h->wide->auto_cap = true;   // keeps doubling, up to 256 states
         }
-        rc = asr_ctc_decode(h->wide, h->last_emis, T, B, h->last_is_log, st);
+        rc = asr_ctc_decode_ex(h->wide, h->last_emis, T, B, h->last_tstride, h->last_ustride,
+                               h->last_lengths.empty() ? nullptr : h->last_lengths.data(),
+                               h->last_is_log, st);
         if (rc) return rc;
         return asr_ctc_get_beams(h->wide, max_hyps, max_len, n_hyps, lengths, labels, logp);
     }

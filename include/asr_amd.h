@@ -137,6 +137,14 @@ int asr_ctc_destroy(asr_ctc_t* h);
  * cu:263).  Fetch results with asr_ctc_get_best / asr_ctc_get_beams. */
 int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, asr_stream_t s);
 
+/* General form (ctcdecode-style batches): element
+ * (t, b, v) of the emissions is d_emis[t*frame_stride + b*utt_stride + v]
+ * (time-major [T][B][V]: B*V, V; batch-major [B][T][V]: V, T*V), and
+ * utterance b has h_lengths[b] <= T frames (host array; NULL = T for all).
+ * asr_ctc_decode(h, e, T, B, is_log, s) is this with time-major strides. */
+int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long frame_stride,
+                      long utt_stride, const int32_t* h_lengths, int is_log, asr_stream_t s);
+
 /* Best hypothesis of each utterance (cpp:74-84: max score, first in string
  * order on ties).  Synchronises the decode stream.  h_labels[B][max_len]
  * (label ids), h_lengths[B], h_logp[B] (fp64 log-probability).
