@@ -38,6 +38,7 @@ ASR_ERR_STATE = 6
 ASR_ERR_INTERNAL = 7
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_LOGSOFTMAX = 0, 1, 2, 3
+SEMANTICS_CPU, SEMANTICS_CUDA = 0, 1   # asr_ctc_set_semantics
 
 # Every symbol include/asr_amd.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
@@ -48,7 +49,7 @@ EXPORTS = [
     "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
     "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
-    "asr_ctc_get_config", "asr_ctc_decode_ex",
+    "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
 ]
 
 
@@ -109,6 +110,7 @@ def lib() -> ctypes.CDLL:
         "asr_ctc_set_waves": [_vp, _i],
         "asr_ctc_get_config": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_ctc_decode_ex": [_vp, _vp, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
+        "asr_ctc_set_semantics": [_vp, _i],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -303,6 +305,11 @@ class CTCDecoder:
 
     def set_waves(self, waves: int) -> None:
         check(lib().asr_ctc_set_waves(self.h, waves), "asr_ctc_set_waves")
+
+    def set_semantics(self, semantics: int) -> None:
+        """SEMANTICS_CPU (default, the parity target) or SEMANTICS_CUDA
+        (CTCBeamSearch.cu: exactly beam states, strip-then-merge last step)."""
+        check(lib().asr_ctc_set_semantics(self.h, semantics), "asr_ctc_set_semantics")
 
     def decode_device(self, d_emis: int, T: int, B: int, is_log: bool, stream: int = 0,
                       lengths: Optional[Sequence[int]] = None, frame_stride: Optional[int] = None,

@@ -25,6 +25,7 @@ struct CtcArgs {
     const int* lengths;     // [B] frames per utterance (device; NULL = T for all)
     int T, B;
     int is_log;
+    int cu_mode;            // 1: CTCBeamSearch.cu semantics (exactly beam states, strip-then-merge last)
     uint64_t blank_less;    // bit c: code(blank) < code(c)   (V <= 64 kernels)
     const int* codes;       // [V] symbol codes (device; wide-vocabulary kernel)
     int4* nodes;            // [B][T*kcap] (parent node, 0, 8 labels packed lo, hi)

@@ -210,6 +210,7 @@ int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float*
 // ---------------------------------------------------------------- CTC handle
 struct asr_ctc {
     int V, beam, blank, K, kcap, waves_override;
+    int cu_mode = 0;                // ASR_CTC_SEMANTICS_CUDA
     std::vector<int32_t> codes;
     uint64_t blank_less;
     int device;
@@ -398,6 +399,16 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     return ASR_OK;
 }
 
+int asr_ctc_set_semantics(asr_ctc_t* h, int semantics) {
+    if (!h || (semantics != ASR_CTC_SEMANTICS_CPU && semantics != ASR_CTC_SEMANTICS_CUDA))
+        return ASR_ERR_ARG;
+    if (semantics == ASR_CTC_SEMANTICS_CUDA && h->V + 1 > 64) return ASR_ERR_UNSUPPORTED;
+    h->cu_mode = semantics == ASR_CTC_SEMANTICS_CUDA ? 1 : 0;
+    h->K = h->cu_mode ? h->beam : h->beam + 1;   // exactly beam states vs beam+1 and ties
+    h->have = false;
+    return ASR_OK;
+}
+
 int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
     if (!h || !(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8)) return ASR_ERR_ARG;
     h->waves_override = waves;
@@ -451,6 +462,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.T = T;
     a.B = B;
     a.is_log = is_log ? 1 : 0;
+    a.cu_mode = h->cu_mode;
     a.blank_less = h->blank_less;
     a.codes = h->d_codes;
     a.nodes = h->d_nodes;
@@ -511,6 +523,8 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
                                     std::min(256, 2 * h->kcap), &h->wide);
             if (rc) return rc;
             h->wide->auto_cap = true;
+            h->wide->cu_mode = h->cu_mode;
+            h->wide->K = h->K;
         }
         int rc = asr_ctc_decode_ex(h->wide, h->last_emis, T, B, h->last_tstride, h->last_ustride,
                                    h->last_lengths.empty() ? nullptr : h->last_lengths.data(),
@@ -564,7 +578,9 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
             rc = asr_ctc_create(h->codes.data(), h->V, h->beam, h->blank, std::min(256, 2 * h->kcap),
                                 &h->wide);
             if (rc) return rc;
-            h->wide->auto_cap = true;   // keeps doubling, up to 256 states
+            h->wide->auto_cap = true;
+            h->wide->cu_mode = h->cu_mode;
+            h->wide->K = h->K;   // keeps doubling, up to 256 states
         }
         rc = asr_ctc_decode_ex(h->wide, h->last_emis, T, B, h->last_tstride, h->last_ustride,
                                h->last_lengths.empty() ? nullptr : h->last_lengths.data(),

@@ -165,6 +165,17 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps
 /* Device time of the last decode's beam-search kernel (ms, HIP events on the
  * decode stream) and its launch geometry; for roofline accounting. */
 int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms);
+/* Search semantics.  ASR_CTC_SEMANTICS_CPU (default):
+ * CTCBeamSearch.cpp with fixes F1-F3 — beam+1 states plus ties at the cutoff,
+ * final "q"/"q$" merge after the last prune; the parity target.
+ * ASR_CTC_SEMANTICS_CUDA: what CTCBeamSearch.cu computes when it works —
+ * exactly min(beam, n) states per step (stable descending sort, cu:174-196;
+ * ties at the cutoff resolved in a fixed slot order instead of the .cu's
+ * string order), and on the last step the trailing blank is stripped before
+ * the merge and the prune (cu:452-456).  V <= 63 only. */
+enum { ASR_CTC_SEMANTICS_CPU = 0, ASR_CTC_SEMANTICS_CUDA = 1 };
+int asr_ctc_set_semantics(asr_ctc_t* h, int semantics);
+
 /* Tuning knobs: waves per utterance (1, 2, 4 or 8; 0 = automatic). */
 int asr_ctc_set_waves(asr_ctc_t* h, int waves);
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes);

@@ -96,3 +96,69 @@ def synthetic_emissions(T: int, B: int, V: int, seed0: int = SEED0, sigma: float
             p = e / e.sum(axis=1, keepdims=True)
         out[:, b, :] = p.astype(np.float32)
     return out
+
+
+def _lse(a: float, b: float) -> float:
+    if a == -np.inf:
+        return b
+    if b == -np.inf:
+        return a
+    m = max(a, b)
+    return m + float(np.log1p(np.exp(-abs(a - b))))
+
+
+def decode_cu(emis: np.ndarray, beam: int, blank: int = 0, codes: Optional[Sequence[int]] = None,
+              is_log: bool = False) -> List[List[Tuple[List[int], float]]]:
+    """Pure-Python restatement of what /root/reference/CTCBeamSearch.cu
+    computes when it works (small cases only):
+      * initialPath (cu:337-401): one state per symbol at t = 0, pruned;
+      * kernelGenNextPaths (cu:404-458): the A.2 transitions; on the last
+        step the trailing blank is stripped per candidate before merging;
+      * merge of identical strings (cu:150-172, 460-489) in string order —
+        the .cu sums with atomicAdd in fp32 (order not fixed); here fp64 log
+        domain, left fold in string order;
+      * prune (cu:174-196, 491-505): stable descending sort of the
+        string-sorted states, exactly min(beam, n) kept.
+    Returns per utterance the final beam [(labels, log p)], best first.
+    States are (labels tuple, ends_in_blank); their string is the code
+    sequence plus code(blank) when ends_in_blank.  T >= 2 (for T = 1 the .cu
+    returns the unstripped initial state)."""
+    T, B, V = emis.shape
+    code = list(range(V)) if codes is None else list(codes)
+    out = []
+    for b in range(B):
+        le = emis[:, b, :].astype(np.float64) if is_log else np.log(emis[:, b, :].astype(np.float64))
+
+        def skey(st):
+            q, fb = st
+            return tuple(code[c] for c in q) + ((code[blank],) if fb else ())
+
+        def prune(states):
+            order = sorted(states.items(), key=lambda kv: skey(kv[0]))       # string order
+            order.sort(key=lambda kv: -kv[1])                                 # stable by score
+            return dict(order[:beam])
+
+        states = {}
+        for c in range(V):
+            st = ((), True) if c == blank else ((c,), False)
+            states[st] = le[0, c]
+        states = prune(states)
+        for t in range(1, T):
+            last = t == T - 1
+            new = {}
+            for (q, fb) in sorted(states, key=skey):
+                s = states[(q, fb)]
+                for c in range(V):
+                    if c == blank:
+                        nst = (q, True)
+                    elif fb or not q or q[-1] != c:
+                        nst = (q + (c,), False)
+                    else:
+                        nst = (q, False)
+                    if last:
+                        nst = (nst[0], False)
+                    new[nst] = _lse(new.get(nst, -np.inf), s + le[t, c])
+            states = prune(new)
+        ranked = sorted(states.items(), key=lambda kv: (-kv[1], skey(kv[0])))
+        out.append([(list(q), float(s)) for (q, _), s in ranked])
+    return out

@@ -1,0 +1,51 @@
+"""CTCBeamSearch.cu semantics mode:
+exactly beam states per step, strip-then-merge on the last step.  Checked
+against the pure-Python restatement oracle.decode_cu and the SURVEY A.6
+golden of the main.cpp vector (".cu emulation": cbacbc, p = 0.0019566051,
+final beam {cbacbc, cbacb})."""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, asr, oracle
+
+
+def test_cu_restatement_matches_survey_golden():
+    g = json.loads((GOLDEN / "main_cpp_ctc.json").read_text())
+    emis = np.array(g["emissions"], np.float32).reshape(g["T"], 1, g["V"])
+    codes = [ord(c) for c in g["vocab"]]
+    res = oracle.decode_cu(emis, g["beam"], g["blank"], codes)[0]
+    names = ["".join(g["vocab"][i] for i in lab) for lab, _ in res]
+    assert names == ["cbacbc", "cbacb"]
+    assert np.exp(res[0][1]) == pytest.approx(0.0019566051, rel=1e-6)
+
+
+@pytest.mark.gpu
+def test_cu_mode_main_cpp_vector():
+    g = json.loads((GOLDEN / "main_cpp_ctc.json").read_text())
+    emis = np.array(g["emissions"], np.float32).reshape(g["T"], 1, g["V"])
+    codes = [ord(c) for c in g["vocab"]]
+    dec = asr.CTCDecoder(g["V"], g["beam"], g["blank"], codes)
+    dec.set_semantics(asr.SEMANTICS_CUDA)
+    dec.decode(emis)
+    beams = dec.beams(8)[0]
+    assert ["".join(g["vocab"][i] for i in lab) for lab, _ in beams] == ["cbacbc", "cbacb"]
+    assert np.exp(beams[0][1]) == pytest.approx(0.0019566051, rel=1e-6)
+    dec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,B,V,beam", [(2, 3, 5, 2), (12, 4, 8, 3), (30, 3, 29, 10), (20, 2, 29, 50)])
+def test_cu_mode_random(T, B, V, beam):
+    emis = oracle.synthetic_emissions(T, B, V, seed0=800 + T + beam)
+    ref = oracle.decode_cu(emis, beam, 0)
+    dec = asr.CTCDecoder(V, beam, 0)
+    dec.set_semantics(asr.SEMANTICS_CUDA)
+    dec.decode(emis)
+    got = dec.beams(dec.config()[0])
+    for b in range(B):
+        assert [l for l, _ in got[b]] == [l for l, _ in ref[b]], f"utterance {b}"
+        for (_, x), (_, y) in zip(got[b], ref[b]):
+            assert abs(x - y) <= 1e-9 * max(1.0, abs(y))
+    dec.close()
