@@ -452,7 +452,9 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
         std::memcpy(h->h_lengths, h_lengths, sizeof(int) * B);
         ASR_HIP_TRY(hipMemcpyAsync(h->d_lengths, h->h_lengths, sizeof(int) * B, hipMemcpyHostToDevice, st0));
     }
-    const int waves = valid_waves(h, h->waves_override ? h->waves_override : auto_waves(h->K));
+    // .cu-semantics kernels exist for the automatic wave count only
+    const int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override
+                                                                       : auto_waves(h->K));
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
