@@ -19,7 +19,7 @@ from __graft_entry__ import PKG, _load  # noqa: E402
 asr = _load("asr_amd", PKG / "asr_amd.py")
 oracle = _load("ctc_oracle", ROOT / "oracle" / "ctc_oracle.py")
 
-PHASES = ["chunk", "P1 cand", "P2a stage1", "P2b exact-lse", "P2c stage2", "P3a scan",
+PHASES = ["chunk", "P1 cand", "P2a folds>=G", "P2b select", "P2c fallback", "P3a scan",
           "P3b+barrier", "P3b max wave", "P3b max wave to desc", "loop:loads+hash", "radix:pre-barrier",
           "radix:barrier", "radix:post", "-", "-", "-"]
 COUNTERS = True   # slots 13-15 of the stamps build are counters
@@ -45,7 +45,7 @@ def run(T, B, V, beam, sigma, waves, reps, stamps):
         per = buf.astype(np.float64).mean(axis=0) / T
         out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(13) if PHASES[i] != "-"}
         ranks = (buf[:, 15] & 0xFFFFFFFF).astype(np.float64)
-        out["per_frame"] = {"stage1_passes": round(per[13], 3), "stage2_passes": round(per[14], 3),
+        out["per_frame"] = {"fallbacks": round(per[13], 4), "exact_passes": round(per[14], 3),
                             "ranks": round(ranks.mean() / T, 3),
                             "mean_cd": round(float((buf[:, 15] >> 32).sum() / max(1.0, ranks.sum())), 2)}
         out["cycles_total"] = round(per[:7].sum(), 1)
