@@ -4,7 +4,11 @@
 
 namespace asr {
 
+#ifdef ASR_CTC_WSTAMPS
+constexpr int NSTAMP = 16 * 8;   // diagnostic: per-wave arrival clocks per utterance
+#else
 constexpr int NSTAMP = 16;   // diagnostic phase clocks per utterance
+#endif
 
 // Launch geometry of one decode, shared by the host planner and the kernel.
 struct CtcGeom {
@@ -52,6 +56,12 @@ constexpr int WIDE_VMAX = 4096;   // largest vocabulary of the wide kernel (ctc_
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
 size_t ctc_lds_bytes_wide(int kc, int V);
 int ctc_set_max_lds_wide();
+// One wave per utterance, list-based (ctc_wave_kernel.inc): the default when supported.
+size_t ctc_lds_bytes_wave(const CtcGeom& g);
+bool ctc_wave_supported(const CtcGeom& g, int cu_mode);
+int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s);
+int ctc_set_max_lds_wave();
+// waves == 0: the one-wave list kernel; 1..8: the workgroup kernel with that many waves.
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s);
 int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);

@@ -250,12 +250,17 @@ struct asr_ctc {
 
 namespace {
 
-// 8 waves per utterance measured fastest at C2/C3; valid_waves
-// lowers it where a narrower instantiation is required.
-int auto_waves(int K) { (void)K; return 8; }
+asr::CtcGeom plan(const asr_ctc* h, int waves);
+
+// Automatic choice: the one-wave list kernel (waves = 0, ctc_wave_kernel.inc)
+// wherever it is instantiated; otherwise 8 waves per utterance, measured
+// fastest of the workgroup kernels at C2/C3.  valid_waves
+// lowers an explicit count where a narrower instantiation is required.
+int auto_waves(const asr_ctc* h) { return asr::ctc_wave_supported(plan(h, 0), h->cu_mode) ? 0 : 8; }
 
 // A (waves, vocab class, rows/thread) combination that ctc_beam_v*.hip instantiates.
 int valid_waves(const asr_ctc* h, int waves) {
+    if (waves == 0) return asr::ctc_wave_supported(plan(h, 0), h->cu_mode) ? 0 : valid_waves(h, 8);
     if (h->V + 1 <= 8 && waves == 8) return 4;   // 8 waves need >= 2 columns per thread
     if (h->kcap > 128 && waves < 4) return 4;   // 4 rows per thread only with 4 or 8 waves
     if (h->V + 1 > 32 && waves == 1) return 2;
@@ -417,10 +422,11 @@ int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
 
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes) {
     if (!h) return ASR_ERR_ARG;
-    const int w = valid_waves(h, h->waves_override ? h->waves_override : auto_waves(h->K));
+    const int w = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h));
     if (max_states) *max_states = h->kcap;
     if (waves) *waves = w;
-    if (lds_bytes) *lds_bytes = (int)asr::ctc_lds_bytes(plan(h, w));
+    if (lds_bytes)
+        *lds_bytes = (int)(w == 0 ? asr::ctc_lds_bytes_wave(plan(h, w)) : asr::ctc_lds_bytes(plan(h, w)));
     return ASR_OK;
 }
 
@@ -454,7 +460,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     }
     // .cu-semantics kernels exist for the automatic wave count only
     const int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override
-                                                                       : auto_waves(h->K));
+                                                                       : auto_waves(h));
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
@@ -476,7 +482,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.best_lab = h->d_best_lab;
     a.best_len = h->d_best_len;
     a.best_score = h->d_best_score;
-#ifdef ASR_CTC_STAMPS
+#if defined(ASR_CTC_STAMPS) || defined(ASR_CTC_WSTAMPS)
     if (h->cap_stamps < B) {
         hipFree(h->d_stamps);
         ASR_HIP_TRY(hipMalloc(&h->d_stamps, sizeof(uint64_t) * asr::NSTAMP * B));
@@ -620,7 +626,7 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
     return stc;
 }
 
-#ifdef ASR_CTC_STAMPS
+#if defined(ASR_CTC_STAMPS) || defined(ASR_CTC_WSTAMPS)
 // Diagnostic build only: per-utterance phase clocks of the last decode.
 int asr_debug_ctc_stamps(asr_ctc_t* h, uint64_t* out) {
     if (!h || !out || !h->have) return ASR_ERR_ARG;

@@ -25,7 +25,11 @@ PHASES = ["chunk", "P1 cand", "P2a folds>=G", "P2b select", "P2c fallback", "P3a
 COUNTERS = True   # slots 13-15 of the stamps build are counters
 
 
-def run(T, B, V, beam, sigma, waves, reps, stamps):
+WPOINTS = {1: "P1 cand", 2: "folds>=G", 3: "select", 4: "fallback/cu", 7: "at offsets barrier",
+           5: "offsets done", 8: "own prefixes", 9: "desc written", 10: "ext built", 6: "frame end"}
+
+
+def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
     emis = oracle.synthetic_emissions(T, B, V, sigma=sigma)
     dec = asr.CTCDecoder(V, beam, 0, waves=waves)
     ms = []
@@ -36,7 +40,29 @@ def run(T, B, V, beam, sigma, waves, reps, stamps):
     out = {"T": T, "B": B, "V": V, "beam": beam, "sigma": sigma, "waves": dec.config()[1],
            "lds": dec.config()[2], "kernel_ms_min": round(min(ms), 4),
            "us_per_frame_step": round(1e3 * min(ms) / T, 3)}
-    if stamps:
+    if wstamps:   # per-wave arrival clocks (libasr_amd_wstamps.so)
+        L = asr.lib()
+        nw = dec.config()[1]
+        buf = np.zeros((B, 8, 16), np.uint64)
+        fn = L.asr_debug_ctc_stamps
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        asr.check(fn(dec.h, buf.ctypes.data), "stamps")
+        frames = buf[:, :nw, 0].astype(np.float64).sum(axis=0)   # per wave
+        per = buf[:, :nw, :].astype(np.float64).sum(axis=0) / frames[:, None]
+        order = sorted(WPOINTS, key=lambda i: per[0, i])
+        out["arrival_cycles_by_wave"] = {WPOINTS[i]: [round(x) for x in per[:, i]] for i in order}
+    if stamps and dec.config()[1] == 0:   # one-wave list kernel: phase clocks and counters
+        L = asr.lib()
+        buf = np.zeros((B, 16), np.uint64)
+        fn = L.asr_debug_ctc_stamps
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        asr.check(fn(dec.h, buf.ctypes.data), "stamps")
+        per = buf.astype(np.float64).mean(axis=0) / T
+        names = ["rows", "own cols", "ext cols", "folds", "select", "survivors", "build", "-",
+                 "M", "live labels", "refills", "fold steps", "-", "xtot", "-", "-"]
+        out["wave_per_frame"] = {names[i]: round(per[i], 2) for i in range(16) if names[i] != "-"}
+        out["cycles_total"] = round(per[:7].sum(), 1)
+    elif stamps:
         L = asr.lib()
         buf = np.zeros((B, 16), np.uint64)
         fn = L.asr_debug_ctc_stamps
@@ -56,6 +82,7 @@ def run(T, B, V, beam, sigma, waves, reps, stamps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--wstamps", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--waves", default="1,2,4")
     ap.add_argument("--cases", default="c2,c3")
@@ -69,7 +96,7 @@ def main():
     for (T, B, V, beam) in ap_cases:
         for sigma in (3.0, 0.5):
             for waves in WAVES:
-                print(json.dumps(run(T, B, V, beam, sigma, waves, args.reps, args.stamps)), flush=True)
+                print(json.dumps(run(T, B, V, beam, sigma, waves, args.reps, args.stamps, args.wstamps)), flush=True)
 
 
 if __name__ == "__main__":

@@ -87,6 +87,21 @@ __global__ void lat(uint64_t* out, int mode, int active_waves) {
             const int a = __builtin_ctz((tid & 63) | 64);   // 0:32 lanes, 1:16, 2:8, ...
             for (int i = 0; i < N; i++) atomicAdd(&buf[a], 1u);
             x = buf[1];
+        } else if (mode == 23) {    // exchange: ds_write_b32 + barrier + dependent ds_read_b32
+            for (int i = 0; i < N; i++) {
+                buf[2048 + (i & 1) * 1024 + tid] = x;
+                __syncthreads();
+                x = buf[2048 + (i & 1) * 1024 + ((tid + 64) & (blockDim.x - 1))] & 63;
+            }
+        } else if (mode == 24) {    // ds_write_b64 x4 + barrier (write drain) + read
+            for (int i = 0; i < N; i++) {
+                b64[(i & 1) * 512 + (tid & 63)] = x;
+                b64[(i & 1) * 512 + 64 + (tid & 63)] = x + 1;
+                b64[(i & 1) * 512 + 128 + (tid & 63)] = x + 2;
+                b64[(i & 1) * 512 + 192 + (tid & 63)] = x + 3;
+                __syncthreads();
+                x = (uint32_t)b64[(i & 1) * 512 + ((tid + 1) & 63)] & 63;
+            }
         } else if (mode == 6) {     // dependent ds_read_b64
             uint64_t y = x;
             for (int i = 0; i < N; i++) y = b64[y & 1023] + (y & 1023);
@@ -94,7 +109,7 @@ __global__ void lat(uint64_t* out, int mode, int active_waves) {
         }
         t1 = __builtin_amdgcn_s_memtime();
     }
-    if (mode == 3 && w >= active_waves)
+    if ((mode == 3 || mode == 23 || mode == 24) && w >= active_waves)
         for (int i = 0; i < N; i++) __syncthreads();
     if ((tid & 63) == 0) out[blockIdx.x * 16 + w] = (t1 - t0) + (x == 0xFFFFFFFFu ? 1 : 0);
 }
@@ -110,12 +125,12 @@ int main() {
                            "ds_max_u64 same addr", "ds_max_u32 same addr", "ds_or_b64 4/addr",
                            "ds_add_u64 same addr", "ds_add_u32 same addr", "ds_add_u32 16 addrs",
                            "ds_add_u32 2x32", "ds_add_u32 48+16", "ds_add_u32 20 lanes 1 addr",
-                           "ds_add_u32 geometric"};
-    for (int mode = 17; mode < 23; mode++)
-        for (int nw : {1, 8}) {
+                           "ds_add_u32 geometric", "write+barrier+read", "4x write_b64+barrier+read"};
+    for (int mode : {0, 1, 6, 3, 23, 24})
+        for (int nw : {1, 2, 4, 8}) {
             for (int rep = 0; rep < 2; rep++) {
                 hipLaunchKernelGGL(lat, dim3(64), dim3(64 * nw), 0, 0, d, mode,
-                                   mode == 3 ? nw : 1);
+                                   (mode == 3 || mode == 23 || mode == 24) ? nw : 1);
                 hipDeviceSynchronize();
             }
             hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
