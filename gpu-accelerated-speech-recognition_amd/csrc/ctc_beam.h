@@ -61,7 +61,7 @@ size_t ctc_lds_bytes_wave(const CtcGeom& g);
 bool ctc_wave_supported(const CtcGeom& g, int cu_mode);
 int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s);
 int ctc_set_max_lds_wave();
-// waves == 0: the one-wave list kernel; 1..8: the workgroup kernel with that many waves.
+// waves < 0: the one-wave list kernel; 1..8: the workgroup kernel with that many waves.
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s);
 int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, in
 }
 
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s) {
-    if (waves == 0) return ctc_launch_decode_wave(a, s);
+    if (waves < 0) return ctc_launch_decode_wave(a, s);
     const int R = a.g.V + 1;
     const int rpt = ctc_row_capacity(a.g.kcap) / 64;   // rows per thread: the layout's KC
     if (R <= 8) return ctc_launch_decode_v8(a, waves, rpt, s);

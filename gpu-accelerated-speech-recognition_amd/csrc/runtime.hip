@@ -252,15 +252,16 @@ namespace {
 
 asr::CtcGeom plan(const asr_ctc* h, int waves);
 
-// Automatic choice: the one-wave list kernel (waves = 0, ctc_wave_kernel.inc)
-// wherever it is instantiated; otherwise 8 waves per utterance, measured
-// fastest of the workgroup kernels at C2/C3.  valid_waves
-// lowers an explicit count where a narrower instantiation is required.
-int auto_waves(const asr_ctc* h) { return asr::ctc_wave_supported(plan(h, 0), h->cu_mode) ? 0 : 8; }
+// Automatic choice: 8 waves per utterance, measured fastest at C2/C3 and on
+// the bench's emissions.  ASR_CTC_WAVES_LIST (-1) selects the
+// one-wave list kernel (ctc_wave_kernel.inc), faster only on peaked
+// emissions.  valid_waves lowers an explicit count where a narrower
+// instantiation is required.
+int auto_waves(const asr_ctc* h) { (void)h; return 8; }
 
 // A (waves, vocab class, rows/thread) combination that ctc_beam_v*.hip instantiates.
 int valid_waves(const asr_ctc* h, int waves) {
-    if (waves == 0) return asr::ctc_wave_supported(plan(h, 0), h->cu_mode) ? 0 : valid_waves(h, 8);
+    if (waves < 0) return asr::ctc_wave_supported(plan(h, 0), h->cu_mode) ? -1 : valid_waves(h, 8);
     if (h->V + 1 <= 8 && waves == 8) return 4;   // 8 waves need >= 2 columns per thread
     if (h->kcap > 128 && waves < 4) return 4;   // 4 rows per thread only with 4 or 8 waves
     if (h->V + 1 > 32 && waves == 1) return 2;
@@ -415,7 +416,9 @@ int asr_ctc_set_semantics(asr_ctc_t* h, int semantics) {
 }
 
 int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
-    if (!h || !(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8)) return ASR_ERR_ARG;
+    if (!h || !(waves == ASR_CTC_WAVES_LIST || waves == 0 || waves == 1 || waves == 2 || waves == 4 ||
+                waves == 8))
+        return ASR_ERR_ARG;
     h->waves_override = waves;
     return ASR_OK;
 }
@@ -426,7 +429,7 @@ int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes
     if (max_states) *max_states = h->kcap;
     if (waves) *waves = w;
     if (lds_bytes)
-        *lds_bytes = (int)(w == 0 ? asr::ctc_lds_bytes_wave(plan(h, w)) : asr::ctc_lds_bytes(plan(h, w)));
+        *lds_bytes = (int)(w < 0 ? asr::ctc_lds_bytes_wave(plan(h, w)) : asr::ctc_lds_bytes(plan(h, w)));
     return ASR_OK;
 }
 

@@ -176,7 +176,11 @@ int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms);
 enum { ASR_CTC_SEMANTICS_CPU = 0, ASR_CTC_SEMANTICS_CUDA = 1 };
 int asr_ctc_set_semantics(asr_ctc_t* h, int semantics);
 
-/* Tuning knobs: waves per utterance (1, 2, 4 or 8; 0 = automatic). */
+/* Tuning knobs: waves per utterance (1, 2, 4 or 8; 0 = automatic), or
+ * ASR_CTC_WAVES_LIST: one wave per utterance with live-label candidate lists
+ * (faster on peaked emissions, slower on flat ones).
+ * get_config reports the schedule a decode will use (ASR_CTC_WAVES_LIST or 1..8). */
+#define ASR_CTC_WAVES_LIST (-1)
 int asr_ctc_set_waves(asr_ctc_t* h, int waves);
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes);
 
