@@ -9,7 +9,9 @@ already resident in HBM:
 Steps are pipelined by default (--no-pipeline: strictly sequential): the RNN
 and emission projection of batch i+1 run on one HIP stream while batch i is
 decoded on another (double-buffered emissions, event-ordered), so the 64
-recurrence workgroups and the 64 decoder workgroups share the 256 CUs.
+recurrence workgroups and the 64 decoder workgroups share the 256 CUs; the
+results of batch i come back in one copy of a packed buffer behind its decode
+(an event wait).
 Every step still does all of its work inside the timed region.
 Default workload = BASELINE.json configs[1] (C2): B=64 utterances per GPU,
 T=500 frames, hidden 256, vocab 29, beam 50.  Multi-GPU: one process per GPU
@@ -110,6 +112,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run RNN and decode of each step back to back on one stream")
+    ap.add_argument("--overlap-results", action="store_true",
+                    help="queue batch i+1's decode before reading batch i's results "
+                         "(measured slower on MI355X: see DESIGN.md §9)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -133,7 +138,10 @@ def main():
     nbuf = 2 if pipeline else 1
     d_hid = [asr.DeviceMatrix(T * B, H) for _ in range(nbuf)]
     d_emis = [asr.DeviceMatrix(T * B, V) for _ in range(nbuf)]
-    dec = asr.CTCDecoder(V, beam, 0, waves=args.waves)
+    # one decoder handle per buffer (with --overlap-results the results of batch
+    # i are read after batch i+1's decode is already queued behind it)
+    decs = [asr.CTCDecoder(V, beam, 0, waves=args.waves) for _ in range(nbuf)]
+    dec = decs[0]
     if pipeline:   # HIP streams/events via torch (same HIP runtime as libasr_amd)
         torch.cuda.set_device(local)
         s_prod, s_dec = torch.cuda.Stream(), torch.cuda.Stream()
@@ -154,12 +162,19 @@ def main():
 
     kernel_ms = []
 
-    def consume(k):
-        """Decode buffer k, traceback, results to the host."""
-        dec.decode_device(d_emis[k].ptr, T, B, is_log=True, stream=dec_stream)
-        labels, lens, lp = dec.best_arrays()   # D2H of the results + decode-stream sync
-        kernel_ms.append(dec.last_kernel_ms())
+    def enqueue(k):
+        """Decode buffer k and its traceback; the results follow to pinned host memory."""
+        decs[k].decode_device(d_emis[k].ptr, T, B, is_log=True, stream=dec_stream)
+
+    def collect(k):
+        """Wait for buffer k's results (an event, not the stream) and read them."""
+        labels, lens, lp = decs[k].best_arrays()
+        kernel_ms.append(decs[k].last_kernel_ms())
         return labels, lp
+
+    def consume(k):
+        enqueue(k)
+        return collect(k)
 
     def run(n):
         """n steps; every step's RNN, projection, decode and result copy."""
@@ -173,6 +188,7 @@ def main():
         with torch.cuda.stream(s_prod):
             produce(0)
             ev_ready[0].record(s_prod)
+        prev = None
         for i in range(n):
             k = i % 2
             if i + 1 < n:   # batch i+1 is produced while batch i is decoded
@@ -181,9 +197,15 @@ def main():
                 produce(kn)
                 ev_ready[kn].record(s_prod)
             s_dec.wait_event(ev_ready[k])
-            out = consume(k)
+            enqueue(k)
             ev_free[k].record(s_dec)
-        return out
+            if not args.overlap_results:
+                out = collect(k)
+                continue
+            if prev is not None:   # batch i-1's results, while batch i decodes
+                out = collect(prev)
+            prev = k
+        return out if prev is None else collect(prev)
 
     run(args.warmup)
     kernel_ms.clear()
@@ -244,7 +266,8 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    dec.close()
+    for d in decs:
+        d.close()
 
 
 if __name__ == "__main__":

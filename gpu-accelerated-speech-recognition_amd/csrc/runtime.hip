@@ -217,16 +217,20 @@ struct asr_ctc {
     // workspace (device)
     int capB = 0, capT = 0;
     int4* d_nodes = nullptr;
-    int *d_fin_n = nullptr, *d_fin_node = nullptr, *d_status = nullptr;
+    int *d_fin_n = nullptr, *d_fin_node = nullptr, *d_status = nullptr;   // d_status: in d_res
     uint64_t* d_fin_tail = nullptr;
     int* d_chain = nullptr;         // traceback scratch [B][2][T/4+1]
     double* d_fin_score = nullptr;
+    // per-decode results, packed so that one copy brings them to the host:
+    // [score f64 x B][len i32 x B][status i32 x B][labels i32 x B x T]
+    unsigned char* d_res = nullptr;
     int *d_best_lab = nullptr, *d_best_len = nullptr;
     double* d_best_score = nullptr;
     int* d_codes = nullptr;
     int *d_all_lab = nullptr, *d_all_len = nullptr;
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
+    unsigned char* h_res = nullptr;   // pinned mirror of d_res
     int *h_best_lab = nullptr, *h_best_len = nullptr, *h_status = nullptr;
     double* h_best_score = nullptr;
     // last decode
@@ -234,6 +238,7 @@ struct asr_ctc {
     int lastT = 0, lastB = 0, last_waves = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_res = nullptr;    // traceback done, results in the pinned mirror
     asr::CtcArgs args{};
     uint64_t* d_stamps = nullptr;   // diagnostic build only
     int cap_stamps = 0;
@@ -283,13 +288,12 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
 }
 
 void free_ws(asr_ctc* h) {
-    hipFree(h->d_nodes); hipFree(h->d_fin_n); hipFree(h->d_fin_node); hipFree(h->d_status);
+    hipFree(h->d_nodes); hipFree(h->d_fin_n); hipFree(h->d_fin_node);
     hipFree(h->d_fin_tail); hipFree(h->d_chain);
     h->d_fin_tail = nullptr; h->d_chain = nullptr;
-    hipFree(h->d_fin_score); hipFree(h->d_best_lab); hipFree(h->d_best_len);
-    hipFree(h->d_best_score);
-    hipHostFree(h->h_best_lab); hipHostFree(h->h_best_len); hipHostFree(h->h_status);
-    hipHostFree(h->h_best_score);
+    hipFree(h->d_fin_score); hipFree(h->d_res);
+    hipHostFree(h->h_res);
+    h->d_res = nullptr; h->h_res = nullptr;
     h->d_nodes = nullptr; h->d_fin_n = h->d_fin_node = h->d_status = nullptr;
     h->d_fin_score = nullptr; h->d_best_lab = h->d_best_len = nullptr; h->d_best_score = nullptr;
     h->h_best_lab = h->h_best_len = h->h_status = nullptr; h->h_best_score = nullptr;
@@ -307,16 +311,11 @@ int ensure_ws(asr_ctc* h, int B, int T) {
     ASR_HIP_TRY(hipMalloc(&h->d_fin_tail, sizeof(uint64_t) * nB * kc));
     ASR_HIP_TRY(hipMalloc(&h->d_chain, sizeof(int) * (size_t)nB * 2 * (nT / 4 + 1)));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_n, sizeof(int) * nB));
-    ASR_HIP_TRY(hipMalloc(&h->d_status, sizeof(int) * nB));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_node, sizeof(int) * nB * kc));
     ASR_HIP_TRY(hipMalloc(&h->d_fin_score, sizeof(double) * nB * kc));
-    ASR_HIP_TRY(hipMalloc(&h->d_best_lab, sizeof(int) * (size_t)nB * nT));
-    ASR_HIP_TRY(hipMalloc(&h->d_best_len, sizeof(int) * nB));
-    ASR_HIP_TRY(hipMalloc(&h->d_best_score, sizeof(double) * nB));
-    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_best_lab, sizeof(int) * (size_t)nB * nT, 0));
-    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_best_len, sizeof(int) * nB, 0));
-    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_status, sizeof(int) * nB, 0));
-    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_best_score, sizeof(double) * nB, 0));
+    const size_t res_bytes = 16 * (size_t)nB + sizeof(int) * (size_t)nB * nT;
+    ASR_HIP_TRY(hipMalloc(&h->d_res, res_bytes));
+    ASR_HIP_TRY(hipHostMalloc((void**)&h->h_res, res_bytes, 0));
     h->capB = nB;
     h->capT = nT;
     return ASR_OK;
@@ -380,7 +379,8 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     if (hipGetDevice(&h->device) != hipSuccess ||
         hipMalloc(&h->d_codes, sizeof(int) * V) != hipSuccess ||
         hipMemcpy(h->d_codes, h->codes.data(), sizeof(int) * V, hipMemcpyHostToDevice) != hipSuccess ||
-        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_res, hipEventDisableTiming) != hipSuccess) {
         delete h;
         return ASR_ERR_HIP;
     }
@@ -401,6 +401,7 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     if (h->wide) asr_ctc_destroy(h->wide);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
+    if (h->ev_res) hipEventDestroy(h->ev_res);
     delete h;
     return ASR_OK;
 }
@@ -481,6 +482,15 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.fin_node = h->d_fin_node;
     a.fin_tail = h->d_fin_tail;
     a.fin_score = h->d_fin_score;
+    // packed result layout for this (B, T)
+    h->d_best_score = reinterpret_cast<double*>(h->d_res);
+    h->d_best_len = reinterpret_cast<int*>(h->d_res + 8 * (size_t)B);
+    h->d_status = reinterpret_cast<int*>(h->d_res + 12 * (size_t)B);
+    h->d_best_lab = reinterpret_cast<int*>(h->d_res + 16 * (size_t)B);
+    h->h_best_score = reinterpret_cast<double*>(h->h_res);
+    h->h_best_len = reinterpret_cast<int*>(h->h_res + 8 * (size_t)B);
+    h->h_status = reinterpret_cast<int*>(h->h_res + 12 * (size_t)B);
+    h->h_best_lab = reinterpret_cast<int*>(h->h_res + 16 * (size_t)B);
     a.status = h->d_status;
     a.best_lab = h->d_best_lab;
     a.best_len = h->d_best_len;
@@ -500,6 +510,12 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     ASR_HIP_TRY(hipEventRecord(h->ev1, st));
     rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, st);
     if (rc) return rc;
+    // One copy of the packed results to the pinned mirror right behind the
+    // traceback: asr_ctc_get_best waits for this event only, not for work the
+    // caller queued on the stream afterwards (e.g. the next batch's decode).
+    ASR_HIP_TRY(hipMemcpyAsync(h->h_res, h->d_res, 16 * (size_t)B + sizeof(int) * (size_t)B * T,
+                               hipMemcpyDeviceToHost, st));
+    ASR_HIP_TRY(hipEventRecord(h->ev_res, st));
     h->have = true;
     h->last_emis = d_emis;
     h->last_tstride = frame_stride;
@@ -517,14 +533,9 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
     if (!h || (!labels && max_len > 0)) return ASR_ERR_ARG;
     if (!h->have) return ASR_ERR_STATE;
     const int B = h->lastB, T = h->lastT;
-    const hipStream_t st = h->stream;
-    ASR_HIP_TRY(hipMemcpyAsync(h->h_best_len, h->d_best_len, sizeof(int) * B, hipMemcpyDeviceToHost, st));
-    ASR_HIP_TRY(hipMemcpyAsync(h->h_best_score, h->d_best_score, sizeof(double) * B, hipMemcpyDeviceToHost, st));
-    ASR_HIP_TRY(hipMemcpyAsync(h->h_status, h->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
-    const int ncol = std::min(T, std::max(max_len, 1));
-    ASR_HIP_TRY(hipMemcpy2DAsync(h->h_best_lab, sizeof(int) * ncol, h->d_best_lab, sizeof(int) * T,
-                                 sizeof(int) * ncol, B, hipMemcpyDeviceToHost, st));
-    ASR_HIP_TRY(hipStreamSynchronize(st));
+    // the decode enqueued the traceback and the copy of its packed results
+    ASR_HIP_TRY(hipEventSynchronize(h->ev_res));
+    const int pitch = T;   // rows of the pinned label mirror
     const int stc = status_code(h->h_status, B);
     if (stc == ASR_ERR_BEAM_OVERFLOW && h->auto_cap && h->kcap < 256) {
         // More ties at the cutoff than room: decode again with twice the
@@ -548,7 +559,7 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
         if (lengths) lengths[b] = len;
         if (logp) logp[b] = h->h_best_score[b];
         if (labels) {
-            const int* fwd = h->h_best_lab + (size_t)b * ncol;
+            const int* fwd = h->h_best_lab + (size_t)b * pitch;
             const int n = std::min(len, max_len);
             for (int i = 0; i < n; i++) labels[(size_t)b * max_len + i] = fwd[i];
         }
