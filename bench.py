@@ -120,6 +120,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; more ranks than GPUs (a rehearsal on a smaller box)
+    # wrap around.  device_count() does not initialise the GPU.
+    ndev = torch.cuda.device_count() if torch is not None else 1
+    local = local % max(1, ndev)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     asr.set_device(local)
