@@ -32,6 +32,9 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
 int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
 int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);
+// MFMA recurrence step (H % 128 == 0); ASR_ERR_UNSUPPORTED otherwise.
+int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
+                         const float* b_hh, int B, int H, hipStream_t s);
 int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                     const float* b_hh, int B, int H, hipStream_t s);
 

@@ -354,6 +354,100 @@ int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b
 }
 
 // ---------------------------------------------------------------------------
+// One recurrence step on MFMA for H % 128 == 0 (C5: H = 1024):
+// h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)) in place over P_t.
+// A workgroup owns a (16*RB rows) x 16 columns tile; its RSM_WAVES (8) waves
+// split K eight ways (H/8 each) so that one step costs ~H/8/4 dependent MFMAs
+// instead of the whole K chain.  No LDS staging: every wave issues all the
+// operand loads of its K slice before its first MFMA (h rows as float4, W_hh
+// columns as 64-B row segments), then one LDS exchange sums the eight
+// partial tiles in a fixed order.  k assignment inside a 16-k chunk: MFMA j
+// of lane group g = lane>>4 takes k = 4g + j for both operands (any
+// bijection is a valid contraction).  Grid (H/16, ceil(B/(16*RB))).
+template <int RB, int RSM_WAVES>
+__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __restrict__ ht,
+                                                                      const float* __restrict__ hp,
+                                                                      const float* __restrict__ Whh,
+                                                                      const float* __restrict__ b_ih,
+                                                                      const float* __restrict__ b_hh,
+                                                                      int B, int H) {
+    __shared__ f32x4 part[RSM_WAVES][RB][64];
+    constexpr int CH = 8;   // 16-k chunks whose loads are in flight together
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n0 = blockIdx.x * 16, r0 = blockIdx.y * (16 * RB);
+    const int g = lane >> 4, c = lane & 15;
+    const int kw = H / RSM_WAVES, kbeg = w * kw, nchunk = kw / 16;
+    const float* arow[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) {
+        const int r = min(r0 + rb * 16 + c, B - 1);   // rows past B: valid memory, never stored
+        arow[rb] = hp + (long)r * H + kbeg + 4 * g;
+    }
+    const float* bcol = Whh + (long)(kbeg + 4 * g) * H + n0 + c;
+    f32x4 acc[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ch0 = 0; ch0 < nchunk; ch0 += CH) {
+        float4 a[CH][RB];
+        float b[CH][4];
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            if (ch0 + i < nchunk) {
+                const int k = (ch0 + i) * 16;
+#pragma unroll
+                for (int rb = 0; rb < RB; rb++) a[i][rb] = *reinterpret_cast<const float4*>(arow[rb] + k);
+#pragma unroll
+                for (int j = 0; j < 4; j++) b[i][j] = bcol[(long)(k + j) * H];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            if (ch0 + i < nchunk) {
+#pragma unroll
+                for (int rb = 0; rb < RB; rb++) {
+                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].x, b[i][0], acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].y, b[i][1], acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].z, b[i][2], acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].w, b[i][3], acc[rb], 0, 0, 0);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) part[w][rb][lane] = acc[rb];
+    __syncthreads();
+    // thread -> (rb, j, lane) of the tile; the C/D layout of 16x16 tiles:
+    // element j of lane l is row (l>>4)*4 + j, column l & 15.
+    for (int e = tid; e < RB * 256; e += 64 * RSM_WAVES) {
+        const int rb = e >> 8, j = (e >> 6) & 3, l = e & 63;
+        const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + (l & 15);
+        if (r >= B) continue;
+        float hh = part[0][rb][l][j];
+#pragma unroll
+        for (int q = 1; q < RSM_WAVES; q++) hh += part[q][rb][l][j];
+        float* out = ht + (long)r * H + n;
+        *out = tanhf((*out + hh) + (b_hh[n] + b_ih[n]));
+    }
+}
+
+int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
+                         const float* b_hh, int B, int H, hipStream_t s) {
+    if (B <= 0 || H <= 0 || (H % 128) != 0) return ASR_ERR_UNSUPPORTED;
+    if ((uintptr_t)hp % 16 != 0) return ASR_ERR_UNSUPPORTED;   // float4 rows
+    const unsigned nb16 = (unsigned)((B + 15) / 16);
+    if ((unsigned)(H / 16) * nb16 <= 512) {   // 16-row tiles while that is <= 2 per CU
+        hipLaunchKernelGGL((rnn_step_mfma_kernel<1, 8>), dim3((unsigned)(H / 16), nb16),
+                           dim3(64 * 8), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
+    } else {   // 32-row tiles (measured: 16-row tiles win up to ~2 workgroups per CU, 64-row
+               // tiles and 16 waves per workgroup lose everywhere)
+        hipLaunchKernelGGL((rnn_step_mfma_kernel<2, 8>), dim3((unsigned)(H / 16), (unsigned)((B + 31) / 32)),
+                           dim3(64 * 8), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
+    }
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // In-place log_softmax of each row of C[M][ldc] (first N columns): one wave
 // per row, max and sum of exp by shuffle reductions.
 __global__ __launch_bounds__(256) void row_logsoftmax_kernel(float* __restrict__ C, long ldc, int M,

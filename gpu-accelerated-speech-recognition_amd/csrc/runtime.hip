@@ -186,13 +186,16 @@ int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float*
     if (rc) return rc;
     // 2. recurrence, in place over hid.
     if (H <= 256) return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
-    // H > 256: one small-M step kernel per frame (W_hh slice per workgroup in
-    // LDS), h_t = tanh((P_t + h_{t-1}.W_hh) + bias) in place.
+    // H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
+    // h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
+    // H % 128 == 0, else the VALU kernel with W_hh slices in LDS.
     for (int t = 0; t < T; t++) {
         float* ht = hid + (size_t)t * B * H;
         const float* hp = t == 0 ? h0 : hid + (size_t)(t - 1) * B * H;
         if (!hp) {   // h_{-1} = 0 (RNN.h:15-16 zero-filled h_0s)
             rc = asr::bias_tanh_launch(ht, b_ih, b_hh, (long)B * H, H, st);
+        } else if ((H & 127) == 0 && ((uintptr_t)hp & 15) == 0) {
+            rc = asr::rnn_step_mfma_launch(ht, hp, W_hh, b_ih, b_hh, B, H, st);
         } else if ((H & 7) == 0) {
             rc = asr::rnn_step_launch(ht, hp, W_hh, b_ih, b_hh, B, H, st);
         } else {   // odd widths: the fused cell GEMM

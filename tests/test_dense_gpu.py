@@ -183,6 +183,26 @@ def test_rnn_forward_c5_hidden():
     close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 1e-4)
 
 
+@pytest.mark.parametrize("T,B,H", [(8, 37, 512), (5, 5, 384), (20, 32, 1024), (4, 16, 128 * 3),
+                                   (6, 100, 512), (3, 256, 1024)])
+def test_rnn_forward_mfma_step(T, B, H):
+    """H % 128 == 0, H > 256: the MFMA recurrence step (8-way K split, ragged
+    batch tiles of 16 and 32 rows), against torch.nn.RNN in fp32."""
+    rng = np.random.default_rng(T * 1000 + B)
+    I = 64
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    hid = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dm(x), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B,
+                h0=dm(h0))
+    close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
+
+
 def test_rnn_multilayer():
     """num_layers > 1 (RNN.h:13-20): layer l+1 consumes layer l's hiddens."""
     T, B, I, H, L = 15, 6, 40, 64, 3
