@@ -47,7 +47,8 @@ EXPORTS = [
     "asr_host_free", "asr_memcpy_h2d", "asr_memcpy_d2h", "asr_memcpy_d2d", "asr_memset",
     "asr_stream_create", "asr_stream_destroy", "asr_stream_sync", "asr_device_sync",
     "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
-    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
+    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
+    "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
 ]
@@ -101,6 +102,7 @@ def lib() -> ctypes.CDLL:
         "asr_linear_fwd": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_cell_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
+        "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
         "asr_ctc_decode": [_vp, _vp, _i, _i, _i, _vp],
@@ -116,6 +118,8 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = _i
+    L.asr_rnn_bidir_workspace_bytes.argtypes = [_i, _i, _i]
+    L.asr_rnn_bidir_workspace_bytes.restype = _sz
     _lib = L
     return L
 
@@ -221,6 +225,26 @@ def rnn_fwd(x: DeviceMatrix, W_ih: DeviceMatrix, W_hh: DeviceMatrix, b_ih: Devic
     check(lib().asr_rnn_fwd(x.ptr, h0.ptr if h0 else None, W_ih.ptr, W_hh.ptr, b_ih.ptr,
                             b_hh.ptr, hid.ptr, T, B, inp, H, stream), "asr_rnn_fwd")
     return hid
+
+
+def rnn_bidir_fwd(x: DeviceMatrix, params: Sequence[Tuple[DeviceMatrix, ...]], out: DeviceMatrix,
+                  T: int, B: int, h0: Optional[DeviceMatrix] = None,
+                  work: Optional["DeviceBytes"] = None, stream: int = 0) -> DeviceMatrix:
+    """nn.RNN(bidirectional=True) (baseline/model.py:30): params[d] = (W_ih, W_hh,
+    b_ih, b_hh) for d = 0 (forward in t) and d = 1 (reverse); h0 [2*B, H];
+    out [T*B, 2H] = (h_fwd, h_bwd) per row."""
+    inp, H = params[0][0].rows, params[0][0].cols
+    assert len(params) == 2 and x.rows == T * B and x.cols == inp
+    assert out.rows == T * B and out.cols == 2 * H
+    need = lib().asr_rnn_bidir_workspace_bytes(T, B, H)
+    if work is None or work.nbytes < need:
+        work = DeviceBytes(need)
+    arr = [(_vp * 2)(*(params[d][k].ptr for d in range(2))) for k in range(4)]
+    check(lib().asr_rnn_bidir_fwd(x.ptr, h0.ptr if h0 else None, arr[0], arr[1], arr[2], arr[3],
+                                  out.ptr, work.ptr, T, B, inp, H, stream), "asr_rnn_bidir_fwd")
+    if stream == 0:
+        check(lib().asr_stream_sync(None), "asr_stream_sync")
+    return out
 
 
 def rnn_cell_fwd(x: DeviceMatrix, h_prev: DeviceMatrix, W_ih: DeviceMatrix,

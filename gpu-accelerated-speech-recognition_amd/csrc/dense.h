@@ -38,4 +38,9 @@ int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const flo
 int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                     const float* b_hh, int B, int H, hipStream_t s);
 
+// Bidirectional RNN plumbing (H % 4 == 0, 16-B aligned buffers).
+int time_reverse_launch(float* p, int T, long n, hipStream_t s);
+int bidir_concat_launch(const float* hf, const float* hr, float* out, int T, int B, int H,
+                        hipStream_t s);
+
 }  // namespace asr

@@ -523,4 +523,53 @@ int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hip
     return ASR_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Bidirectional RNN plumbing (nn.RNN(bidirectional=True), model.py:30).
+// In-place time reversal of a time-major [T][n] buffer: swap rows t and T-1-t.
+__global__ __launch_bounds__(256) void time_reverse_kernel(float4* __restrict__ p, int T, long n4) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;   // over (T/2) * n4
+    if (i >= (long)(T / 2) * n4) return;
+    const long t = i / n4, k = i - t * n4;
+    float4* a = p + t * n4 + k;
+    float4* b = p + (long)(T - 1 - t) * n4 + k;
+    const float4 va = *a, vb = *b;
+    *a = vb;
+    *b = va;
+}
+
+// out[t][b][0:H] = hf[t][b][:], out[t][b][H:2H] = hr[T-1-t][b][:]  (H % 4 == 0, float4 units).
+__global__ __launch_bounds__(256) void bidir_concat_kernel(const float4* __restrict__ hf,
+                                                           const float4* __restrict__ hr,
+                                                           float4* __restrict__ out, int T, int B,
+                                                           int H4) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;   // over T * B * 2 * H4 outputs
+    const long rowlen = 2L * H4;
+    if (i >= (long)T * B * rowlen) return;
+    const long row = i / rowlen;
+    const int j = (int)(i - row * rowlen);
+    const long t = row / B, b = row - t * B;
+    out[i] = j < H4 ? hf[row * H4 + j] : hr[((long)(T - 1 - t) * B + b) * H4 + (j - H4)];
+}
+
+int time_reverse_launch(float* p, int T, long n, hipStream_t s) {
+    if (T < 2 || n <= 0) return ASR_OK;
+    if ((n & 3) || ((uintptr_t)p & 15)) return ASR_ERR_UNSUPPORTED;
+    const long work = (long)(T / 2) * (n / 4);
+    hipLaunchKernelGGL(time_reverse_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<float4*>(p), T, n / 4);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+int bidir_concat_launch(const float* hf, const float* hr, float* out, int T, int B, int H,
+                        hipStream_t s) {
+    if ((H & 3) || (((uintptr_t)hf | (uintptr_t)hr | (uintptr_t)out) & 15)) return ASR_ERR_UNSUPPORTED;
+    const long work = (long)T * B * 2 * (H / 4);
+    hipLaunchKernelGGL(bidir_concat_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(hf), reinterpret_cast<const float4*>(hr),
+                       reinterpret_cast<float4*>(out), T, B, H / 4);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
 }  // namespace asr

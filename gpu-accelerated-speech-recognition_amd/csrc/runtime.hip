@@ -174,17 +174,11 @@ int asr_rnn_cell_fwd(const float* x, const float* h_prev, const float* W_ih, con
     g.b1 = b_ih; g.b2 = b_hh;
     return asr::gemm_launch(g, asr::EPI_DUAL_TANH, asr_stream(s));
 }
-int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float* W_hh,
-                const float* b_ih, const float* b_hh, float* hid, int T, int B, int in, int H,
-                asr_stream_t s) {
-    if (!x || !W_ih || !W_hh || !b_ih || !b_hh || !hid || T <= 0 || B <= 0 || in <= 0 || H <= 0)
-        return ASR_ERR_ARG;
-    if (x == hid) return ASR_ERR_ARG;
-    const hipStream_t st = asr_stream(s);
-    // 1. input projection for all T at once: hid = x . W_ih   ([T*B, in] x [in, H])
-    int rc = asr::gemm_launch(gemm_args(x, W_ih, hid, T * B, in, H), asr::EPI_NONE, st);
-    if (rc) return rc;
-    // 2. recurrence, in place over hid.
+// Recurrence over a hid buffer that already holds the input projection
+// P_t = x_t . W_ih, in place: hid[t] = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)).
+static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
+                          const float* b_hh, float* hid, int T, int B, int H, hipStream_t st) {
+    int rc = ASR_OK;
     if (H <= 256) return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
     // H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
     // h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
@@ -206,6 +200,71 @@ int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float*
         if (rc) return rc;
     }
     return ASR_OK;
+}
+
+int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float* W_hh,
+                const float* b_ih, const float* b_hh, float* hid, int T, int B, int in, int H,
+                asr_stream_t s) {
+    if (!x || !W_ih || !W_hh || !b_ih || !b_hh || !hid || T <= 0 || B <= 0 || in <= 0 || H <= 0)
+        return ASR_ERR_ARG;
+    if (x == hid) return ASR_ERR_ARG;
+    const hipStream_t st = asr_stream(s);
+    // 1. input projection for all T at once: hid = x . W_ih   ([T*B, in] x [in, H])
+    int rc = asr::gemm_launch(gemm_args(x, W_ih, hid, T * B, in, H), asr::EPI_NONE, st);
+    if (rc) return rc;
+    // 2. recurrence, in place over hid.
+    return rnn_recurrence(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+}
+
+size_t asr_rnn_bidir_workspace_bytes(int T, int B, int H) {
+    if (T <= 0 || B <= 0 || H <= 0) return 0;
+    return 2 * (size_t)T * B * H * sizeof(float);
+}
+
+int asr_rnn_bidir_fwd(const float* x, const float* h0, const float* const W_ih[2],
+                      const float* const W_hh[2], const float* const b_ih[2],
+                      const float* const b_hh[2], float* out, void* work, int T, int B, int in,
+                      int H, asr_stream_t s) {
+    if (!x || !W_ih || !W_hh || !b_ih || !b_hh || !out || !work || T <= 0 || B <= 0 || in <= 0 ||
+        H <= 0)
+        return ASR_ERR_ARG;
+    for (int d = 0; d < 2; d++)
+        if (!W_ih[d] || !W_hh[d] || !b_ih[d] || !b_hh[d]) return ASR_ERR_ARG;
+    if ((H & 3) || (((uintptr_t)out | (uintptr_t)work) & 15)) return ASR_ERR_UNSUPPORTED;
+    const size_t n = (size_t)T * B * H;
+    float* hf = static_cast<float*>(work);
+    float* hr = hf + n;
+    if ((const float*)out == x || (hf < x + (size_t)T * B * in && x < hr + n)) return ASR_ERR_ARG;
+    const hipStream_t st = asr_stream(s);
+    // Both input projections on the caller's stream (one GEMM each, full chip);
+    // the reverse direction's P is then flipped in time so that its recurrence
+    // is the forward recurrence over hr.
+    int rc = asr::gemm_launch(gemm_args(x, W_ih[0], hf, T * B, in, H), asr::EPI_NONE, st);
+    if (!rc) rc = asr::gemm_launch(gemm_args(x, W_ih[1], hr, T * B, in, H), asr::EPI_NONE, st);
+    if (!rc) rc = asr::time_reverse_launch(hr, T, (long)B * H, st);
+    if (rc) return rc;
+    // The two recurrences are independent and each is latency-bound on a few
+    // CUs: the reverse one runs on a side stream of this device.
+    static thread_local hipStream_t side[64] = {};
+    static thread_local hipEvent_t ev_fork[64] = {}, ev_join[64] = {};
+    int dev = 0;
+    ASR_HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return ASR_ERR_UNSUPPORTED;
+    if (!side[dev]) {
+        ASR_HIP_TRY(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
+        ASR_HIP_TRY(hipEventCreateWithFlags(&ev_fork[dev], hipEventDisableTiming));
+        ASR_HIP_TRY(hipEventCreateWithFlags(&ev_join[dev], hipEventDisableTiming));
+    }
+    ASR_HIP_TRY(hipEventRecord(ev_fork[dev], st));
+    ASR_HIP_TRY(hipStreamWaitEvent(side[dev], ev_fork[dev], 0));
+    rc = rnn_recurrence(h0 ? h0 + (size_t)B * H : nullptr, W_hh[1], b_ih[1], b_hh[1], hr, T, B, H,
+                        side[dev]);
+    ASR_HIP_TRY(hipEventRecord(ev_join[dev], side[dev]));
+    if (rc) return rc;
+    rc = rnn_recurrence(h0, W_hh[0], b_ih[0], b_hh[0], hf, T, B, H, st);
+    ASR_HIP_TRY(hipStreamWaitEvent(st, ev_join[dev], 0));
+    if (rc) return rc;
+    return asr::bidir_concat_launch(hf, hr, out, T, B, H, st);
 }
 
 }  // extern "C"

@@ -113,6 +113,22 @@ int asr_rnn_fwd(const float* d_x, const float* d_h0, const float* d_W_ih, const 
                 const float* d_b_ih, const float* d_b_hh, float* d_hiddens, int T, int B,
                 int in, int H, asr_stream_t s);
 
+/* Bidirectional single-layer RNN — nn.RNN(bidirectional=True) of the Python
+ * baseline (baseline/model.py:30, "bidir true"); the C++
+ * RNN class (RNN.h:13-20) has no such mode, so this is an added entry point.
+ * Direction d = 0 runs t = 0..T-1, d = 1 runs t = T-1..0, each with its own
+ * W_ih[d] [in,H], W_hh[d] [H,H], b_ih[d], b_hh[d] (RNN_Cell layout).
+ * h0: [2][B][H] (NULL = zeros).  out: [T*B, 2H] time-major, row = (h_fwd, h_bwd)
+ * as torch concatenates them.  work: device scratch of
+ * asr_rnn_bidir_workspace_bytes(T,B,H) bytes, 16-B aligned; H % 4 == 0.  The
+ * two recurrences run concurrently (the reverse one on a library side stream
+ * joined back into s). */
+size_t asr_rnn_bidir_workspace_bytes(int T, int B, int H);
+int asr_rnn_bidir_fwd(const float* d_x, const float* d_h0, const float* const d_W_ih[2],
+                      const float* const d_W_hh[2], const float* const d_b_ih[2],
+                      const float* const d_b_hh[2], float* d_out, void* d_work, int T, int B,
+                      int in, int H, asr_stream_t s);
+
 /* ---- CTC prefix beam search: replaces CTCBeamSearch (CTCBeamSearch.h:107-150,
  *      CTCBeamSearch.cu:220-312) with the semantics of the CPU decoder
  *      CTCBeamSearch.cpp:50-187 (fixes F1-F3, fp64 log domain). ---- */

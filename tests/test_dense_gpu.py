@@ -227,3 +227,35 @@ def test_rnn_multilayer():
             getattr(ref, f"bias_hh_l{l}").copy_(torch.from_numpy(b_hh))
         y, _ = ref(torch.from_numpy(x.reshape(T, B, I)))
     close(out, y.reshape(T * B, H).numpy(), 5e-5)
+
+
+@pytest.mark.parametrize("T,B,I,H,with_h0", [(20, 3, 10, 48, False), (50, 64, 256, 256, True),
+                                             (12, 4, 24, 300, True), (9, 5, 40, 384, False),
+                                             (1, 2, 8, 4, True)])
+def test_rnn_bidirectional(T, B, I, H, with_h0):
+    """nn.RNN(bidirectional=True) (baseline/model.py:30 "bidir true"): out row =
+    (h_fwd[t], h_bwd[t]); torch fp32 on the CPU is the reference.  Covers the
+    register-resident (H <= 256), VALU-step (H=300) and MFMA-step (H=384)
+    recurrences, and T = 1."""
+    rng = np.random.default_rng(1000 + H)
+    s = 1 / np.sqrt(H)
+    params = [(rng.uniform(-s, s, (I, H)).astype(np.float32),
+               rng.uniform(-s, s, (H, H)).astype(np.float32),
+               rng.uniform(-0.1, 0.1, H).astype(np.float32),
+               rng.uniform(-0.1, 0.1, H).astype(np.float32)) for _ in range(2)]
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (2 * B, H)).astype(np.float32) if with_h0 else None
+    out = asr.DeviceMatrix(T * B, 2 * H)
+    dev = [tuple(dm(a if a.ndim == 2 else a.reshape(H, 1)) for a in p) for p in params]
+    asr.rnn_bidir_fwd(dm(x), dev, out, T, B, h0=dm(h0) if with_h0 else None)
+    ref = torch.nn.RNN(I, H, 1, bidirectional=True)
+    with torch.no_grad():
+        for d, sfx in enumerate(["", "_reverse"]):
+            w_ih, w_hh, b_ih, b_hh = params[d]
+            getattr(ref, f"weight_ih_l0{sfx}").copy_(torch.from_numpy(w_ih.T))
+            getattr(ref, f"weight_hh_l0{sfx}").copy_(torch.from_numpy(w_hh.T))
+            getattr(ref, f"bias_ih_l0{sfx}").copy_(torch.from_numpy(b_ih))
+            getattr(ref, f"bias_hh_l0{sfx}").copy_(torch.from_numpy(b_hh))
+        y, _ = ref(torch.from_numpy(x.reshape(T, B, I)),
+                   None if h0 is None else torch.from_numpy(h0.reshape(2, B, H)))
+    close(out.toCpu(), y.reshape(T * B, 2 * H).numpy(), 1e-4)
