@@ -472,6 +472,8 @@ class CTCBeamDecoder:
         if hasattr(probs, "is_cuda") and probs.is_cuda:   # torch GPU tensor: zero-copy
             import torch
             p = probs if probs.dtype == torch.float32 else probs.float()
+            if p.stride(2) != 1:   # the kernel reads a frame's V labels contiguously
+                p = p.contiguous()
             self._dec.decode_device(p.data_ptr(), T, B, self.log_probs_input,
                                     torch.cuda.current_stream().cuda_stream, lens,
                                     p.stride(1), p.stride(0))

@@ -38,10 +38,6 @@ int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const flo
 int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                     const float* b_hh, int B, int H, hipStream_t s);
 
-// Persistent recurrence over frames t0..T-1 (B <= 32, H % 128 == 0, all H/16
-// workgroups co-resident); *err set if a grid-barrier wait timed out.
-int rnn_persist_launch(float* hid, const float* Whh, const float* b_ih, const float* b_hh, int t0,
-                       int T, int B, int H, unsigned* ctr, int* err, hipStream_t s);
 // Bidirectional RNN plumbing (H % 4 == 0, 16-B aligned buffers).
 int time_reverse_launch(float* p, int T, long n, hipStream_t s);
 int bidir_concat_launch(const float* hf, const float* hr, float* out, int T, int B, int H,

@@ -4,7 +4,7 @@
 //    CDNA4) with fused epilogues — replaces cublasSgemm + the ReLU / Tanh
 //    kernels of the reference (cuMatrix.cpp:33-70, Linear.cu:3-10,
 //    RNN_Cell.cu:5-13);
-//  * a persistent RNN recurrence that keeps W_hh in registers for the whole
+//  * an RNN recurrence that keeps W_hh in registers for the whole
 //    sequence (H <= 256), one workgroup per utterance (RNN.cu:9-30 ran
 //    2 GEMMs + a GEAM + a kernel + 3 host syncs per step);
 //  * z = x + lambda*y (matrixAdd, cuMatrix.cpp:147-168).
@@ -443,132 +443,6 @@ int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const flo
         hipLaunchKernelGGL((rnn_step_mfma_kernel<2, 8>), dim3((unsigned)(H / 16), (unsigned)((B + 31) / 32)),
                            dim3(64 * 8), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
     }
-    ASR_LAUNCH_TRY();
-    return ASR_OK;
-}
-
-// ---------------------------------------------------------------------------
-// Persistent recurrence for H % 128 == 0, B <= 32 (C5: H = 1024, B = 32):
-// one launch covers frames t0..T-1.  Workgroup x owns columns [16x, 16x+16)
-// of W_hh, resident in LDS for the whole sequence as float4 quads
-// (quad (k/4, c) holds W[k..k+3][c], so a wave's B-operand read is one
-// contiguous ds_read_b128 per lane).  Per frame: the same 8-way K split and
-// MFMA chain as rnn_step_mfma_kernel, then h_t is published and a grid
-// barrier (agent-scope release, one counter add per workgroup, bounded wait,
-// agent-scope acquire) orders it before frame t+1 reads it.  All H/16
-// workgroups must be co-resident (one per CU; the launcher checks
-// occupancy); a wait that exceeds its bound sets *err and ends the kernel,
-// so a missing workgroup cannot hang the GPU.
-__global__ __launch_bounds__(512) void rnn_persist_kernel(float* __restrict__ hid,
-                                                          const float* __restrict__ Whh,
-                                                          const float* __restrict__ b_ih,
-                                                          const float* __restrict__ b_hh,
-                                                          int t0, int T, int B, int H,
-                                                          unsigned* ctr, int* err) {
-    extern __shared__ float4 wq[];                 // [H/4][16] quads
-    f32x4* part = reinterpret_cast<f32x4*>(wq + (H / 4) * 16);   // [8][2][64]
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n0 = blockIdx.x * 16, G = gridDim.x;
-    const int g = lane >> 4, c = lane & 15;
-    const int kw = H / 8, kbeg = w * kw, nchunk = kw / 16;
-    for (int i = tid; i < (H / 4) * 16; i += 512) {
-        const int kq = i >> 4, cc = i & 15;
-        const float* src = Whh + (long)(4 * kq) * H + n0 + cc;
-        wq[i] = make_float4(src[0], src[H], src[2 * H], src[3 * H]);
-    }
-    // epilogue element of this thread: (rb, j, l) -> row, column (C/D layout)
-    const int rb_e = tid >> 8, j_e = (tid >> 6) & 3, l_e = tid & 63;
-    const int r_e = rb_e * 16 + (l_e >> 4) * 4 + j_e, n_e = n0 + (l_e & 15);
-    const float bias = b_hh[n_e] + b_ih[n_e];
-    __syncthreads();
-    for (int t = t0; t < T; t++) {
-        const float* hp = hid + (long)(t - 1) * B * H;
-        float* ht = hid + (long)t * B * H;
-        const float* arow[2];
-#pragma unroll
-        for (int rb = 0; rb < 2; rb++)
-            arow[rb] = hp + (long)min(rb * 16 + c, B - 1) * H + kbeg + 4 * g;
-        const float pt = r_e < B ? ht[(long)r_e * H + n_e] : 0.f;
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        for (int ch0 = 0; ch0 < nchunk; ch0 += 8) {
-            float4 a[8][2];
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-                if (ch0 + i < nchunk) {
-#pragma unroll
-                    for (int rb = 0; rb < 2; rb++)
-                        a[i][rb] = *reinterpret_cast<const float4*>(arow[rb] + (ch0 + i) * 16);
-                }
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-                if (ch0 + i < nchunk) {
-                    const int kq = (kbeg + (ch0 + i) * 16) / 4 + g;
-                    const float4 b = wq[kq * 16 + c];
-#pragma unroll
-                    for (int rb = 0; rb < 2; rb++) {
-                        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].x, b.x, acc[rb], 0, 0, 0);
-                        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].y, b.y, acc[rb], 0, 0, 0);
-                        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].z, b.z, acc[rb], 0, 0, 0);
-                        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].w, b.w, acc[rb], 0, 0, 0);
-                    }
-                }
-        }
-#pragma unroll
-        for (int rb = 0; rb < 2; rb++) part[(w * 2 + rb) * 64 + lane] = acc[rb];
-        __syncthreads();
-        if (r_e < B) {
-            float hh = part[rb_e * 64 + l_e][j_e];
-#pragma unroll
-            for (int q = 1; q < 8; q++) hh += part[(q * 2 + rb_e) * 64 + l_e][j_e];
-            ht[(long)r_e * H + n_e] = tanhf((pt + hh) + bias);
-        }
-        if (t + 1 == T) break;
-        // grid barrier: h_t of every workgroup before frame t+1.  Every wave
-        // drains its own stores to L2; one thread then releases (L2 write
-        // back), counts in, waits, and acquires (L2 + L1 invalidate, shared
-        // by all waves of this CU).
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            const unsigned target = (unsigned)G * (unsigned)(t - t0 + 1);
-            __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int spins = 0;
-            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1 << 22)) {
-                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
-            __threadfence();
-            reinterpret_cast<volatile int*>(part)[0] = spins > (1 << 22);
-        }
-        __syncthreads();
-        const int bail = reinterpret_cast<volatile int*>(part)[0];
-        __syncthreads();   // part[] is reused by the next frame
-        if (bail) return;
-    }
-}
-
-size_t rnn_persist_lds(int H) { return (size_t)(H / 4) * 16 * 16 + 8 * 2 * 64 * 16; }
-
-int rnn_persist_launch(float* hid, const float* Whh, const float* b_ih, const float* b_hh, int t0,
-                       int T, int B, int H, unsigned* ctr, int* err, hipStream_t s) {
-    if (B <= 0 || B > 32 || (H % 128) != 0 || t0 < 1 || t0 >= T) return ASR_ERR_UNSUPPORTED;
-    if ((uintptr_t)hid % 16 != 0) return ASR_ERR_UNSUPPORTED;
-    const size_t lds = rnn_persist_lds(H);
-    if (lds > 160u * 1024u) return ASR_ERR_UNSUPPORTED;
-    int dev = 0, ncu = 0, per_cu = 0;
-    ASR_HIP_TRY(hipGetDevice(&dev));
-    ASR_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)rnn_persist_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    ASR_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rnn_persist_kernel, 512, lds));
-    if (per_cu < 1 || H / 16 > ncu * per_cu) return ASR_ERR_UNSUPPORTED;
-    ASR_HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(unsigned), s));
-    hipLaunchKernelGGL(rnn_persist_kernel, dim3((unsigned)(H / 16)), dim3(512), lds, s, hid, Whh,
-                       b_ih, b_hh, t0, T, B, H, ctr, err);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

@@ -176,63 +176,9 @@ int asr_rnn_cell_fwd(const float* x, const float* h_prev, const float* W_ih, con
 }
 // Recurrence over a hid buffer that already holds the input projection
 // P_t = x_t . W_ih, in place: hid[t] = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)).
-// Persistent recurrence (opt-in, ASR_RNN_PERSIST=1): frames 1..T-1 in one
-// launch.  Each call takes its own grid-barrier counter from a per-device pool
-// (concurrent calls, e.g. the two directions of asr_rnn_bidir_fwd, must not
-// share one); a barrier timeout is reported as ASR_ERR_HIP after a stream sync.
-static int rnn_persist(float* hid, const float* W_hh, const float* b_ih, const float* b_hh, int T,
-                       int B, int H, hipStream_t st) {
-    constexpr int NSLOT = 64;
-    static unsigned* ctr[64] = {};
-    static int* err[64] = {};
-    static int* h_err[64] = {};
-    static std::atomic<unsigned> next[64];
-    int dev = 0;
-    ASR_HIP_TRY(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return ASR_ERR_UNSUPPORTED;
-    static std::mutex mu;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!ctr[dev]) {
-            void* p = nullptr;
-            ASR_HIP_TRY(hipMalloc(&p, NSLOT * (sizeof(unsigned) + sizeof(int))));
-            ASR_HIP_TRY(hipMemset(p, 0, NSLOT * (sizeof(unsigned) + sizeof(int))));
-            ASR_HIP_TRY(hipHostMalloc((void**)&h_err[dev], NSLOT * sizeof(int), 0));
-            ctr[dev] = static_cast<unsigned*>(p);
-            err[dev] = reinterpret_cast<int*>(ctr[dev] + NSLOT);
-        }
-    }
-    const unsigned k = next[dev].fetch_add(1) % NSLOT;
-    int rc = asr::rnn_persist_launch(hid, W_hh, b_ih, b_hh, 1, T, B, H, ctr[dev] + k, err[dev] + k, st);
-    if (rc) return rc;
-    ASR_HIP_TRY(hipMemcpyAsync(h_err[dev] + k, err[dev] + k, sizeof(int), hipMemcpyDeviceToHost, st));
-    ASR_HIP_TRY(hipStreamSynchronize(st));
-    if (h_err[dev][k]) {
-        ASR_HIP_TRY(hipMemsetAsync(err[dev] + k, 0, sizeof(int), st));
-        asr_internal_set_error("rnn_persist_kernel", "grid barrier wait timed out", __FILE__, __LINE__);
-        return ASR_ERR_HIP;
-    }
-    return ASR_OK;
-}
-
 static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
                           const float* b_hh, float* hid, int T, int B, int H, hipStream_t st) {
     int rc = ASR_OK;
-    static const bool persist = getenv("ASR_RNN_PERSIST") && atoi(getenv("ASR_RNN_PERSIST")) > 0;
-    if (persist && H > 256 && (H & 127) == 0 && B <= 32 && T > 1 && ((uintptr_t)hid & 15) == 0) {
-        // frame 0 as in the step path, then frames 1..T-1 in one launch
-        if (!h0) rc = asr::bias_tanh_launch(hid, b_ih, b_hh, (long)B * H, H, st);
-        else if (((uintptr_t)h0 & 15) == 0) rc = asr::rnn_step_mfma_launch(hid, h0, W_hh, b_ih, b_hh, B, H, st);
-        else rc = asr::rnn_step_launch(hid, h0, W_hh, b_ih, b_hh, B, H, st);
-        if (rc) return rc;
-        rc = rnn_persist(hid, W_hh, b_ih, b_hh, T, B, H, st);
-        if (rc != ASR_ERR_UNSUPPORTED) return rc;
-        rc = ASR_OK;   // not co-resident on this device: the per-frame kernels below
-        for (int t = 1; t < T && !rc; t++)
-            rc = asr::rnn_step_mfma_launch(hid + (size_t)t * B * H, hid + (size_t)(t - 1) * B * H,
-                                           W_hh, b_ih, b_hh, B, H, st);
-        return rc;
-    }
     if (H <= 256) return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
     // H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
     // h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
@@ -313,9 +259,15 @@ int asr_rnn_bidir_fwd(const float* x, const float* h0, const float* const W_ih[2
     ASR_HIP_TRY(hipStreamWaitEvent(side[dev], ev_fork[dev], 0));
     rc = rnn_recurrence(h0 ? h0 + (size_t)B * H : nullptr, W_hh[1], b_ih[1], b_hh[1], hr, T, B, H,
                         side[dev]);
-    ASR_HIP_TRY(hipEventRecord(ev_join[dev], side[dev]));
-    if (rc) return rc;
-    rc = rnn_recurrence(h0, W_hh[0], b_ih[0], b_hh[0], hf, T, B, H, st);
+    // Join the side stream back into the caller's stream on every path,
+    // errors included: kernels already queued there still write `work`,
+    // which the caller may free once this returns.
+    const hipError_t je = hipEventRecord(ev_join[dev], side[dev]);
+    if (je != hipSuccess) {
+        hipStreamSynchronize(side[dev]);
+        ASR_HIP_TRY(je);
+    }
+    if (!rc) rc = rnn_recurrence(h0, W_hh[0], b_ih[0], b_hh[0], hf, T, B, H, st);
     ASR_HIP_TRY(hipStreamWaitEvent(st, ev_join[dev], 0));
     if (rc) return rc;
     return asr::bidir_concat_launch(hf, hr, out, T, B, H, st);

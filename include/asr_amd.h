@@ -150,7 +150,12 @@ int asr_ctc_destroy(asr_ctc_t* h);
  * utterances of d_emis[T][B][V] (probabilities, or log-probabilities if
  * is_log).  Enqueues the decode and the best-path traceback on stream s; the
  * workspace is sized once and reused (the reference re-allocated per call,
- * cu:263).  Fetch results with asr_ctc_get_best / asr_ctc_get_beams. */
+ * cu:263).  Fetch results with asr_ctc_get_best / asr_ctc_get_beams.
+ * Lifetime: d_emis must stay allocated and unmodified until the results of
+ * this decode have been fetched (asr_ctc_get_best / asr_ctc_get_beams
+ * returned), because an automatic-capacity handle re-decodes it when ties
+ * at the cutoff overflow the beam (see asr_ctc_get_best).  Work the caller
+ * queues that writes d_emis must be ordered after that fetch. */
 int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, asr_stream_t s);
 
 /* General form (ctcdecode-style batches): element

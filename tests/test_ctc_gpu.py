@@ -156,3 +156,29 @@ def test_c2_shape_best():
         assert abs(lp[b] - ref[b][0][1]) <= TOL * abs(ref[b][0][1])
     beams = dec.beams(beam + 1)
     assert_beams_equal([x[:beam + 1] for x in beams[:8]], [r[:beam + 1] for r in ref[:8]], "C2")
+
+
+def test_overflow_retry_with_next_batch_queued():
+    """An automatic-capacity handle whose decode overflows (more tied
+    survivors than max_states) re-decodes the caller's emission buffer when
+    the results are fetched (asr_amd.h lifetime rule: the buffer stays valid
+    and unmodified until then).  Here another handle's decode of a different
+    buffer is queued on the same stream before the overflowing results are
+    read; both results must still be the oracle's."""
+    T, V, beam = 4, 5, 5
+    uni = np.full((T, 2, V), 1.0 / V, np.float32)
+    ref_u = oracle.decode(uni, beam, 0, max_hyps=4096)
+    other = oracle.synthetic_emissions(30, 3, V, seed0=31)
+    ref_o = oracle.decode(other, beam, 0)
+    dA = asr.DeviceMatrix.from_numpy(uni.reshape(T * 2, V))
+    dB = asr.DeviceMatrix.from_numpy(other.reshape(30 * 3, V))
+    h1, h2 = asr.CTCDecoder(V, beam, 0), asr.CTCDecoder(V, beam, 0)
+    assert h1.config()[0] < max(len(r) for r in ref_u)   # the default capacity overflows
+    h1.decode_device(dA.ptr, T, 2, is_log=False)
+    h2.decode_device(dB.ptr, 30, 3, is_log=False)         # next batch queued first
+    best1, lp1 = h1.best()
+    assert best1 == [r[0][0] for r in ref_u]
+    assert_beams_equal(h1.beams(max_hyps=4096), ref_u, "overflow retry")
+    assert_beams_equal(h2.beams(max_hyps=h2.config()[0]), ref_o, "next batch")
+    h1.close()
+    h2.close()

@@ -259,3 +259,22 @@ def test_rnn_bidirectional(T, B, I, H, with_h0):
         y, _ = ref(torch.from_numpy(x.reshape(T, B, I)),
                    None if h0 is None else torch.from_numpy(h0.reshape(2, B, H)))
     close(out.toCpu(), y.reshape(T * B, 2 * H).numpy(), 1e-4)
+
+
+def test_rnn_forward_h2048():
+    """The reference harness's hidden size (baseline/config.json:7,
+    rnn_hidden_size 2048; in = linear_size 2048): MFMA recurrence step at
+    H = 2048 against torch.nn.RNN in fp32."""
+    T, B, I, H = 6, 8, 2048, 2048
+    rng = np.random.default_rng(2048)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    hid = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dm(x), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B,
+                h0=dm(h0))
+    close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)

@@ -2,21 +2,24 @@
 
 Utterances shard contiguously over ranks with no data-path collective; each
 rank's inputs are generated per utterance so shards reproduce the full batch;
-the host gathers the hypotheses.  Checked here with the CPU oracle standing
-in for each rank's decoder, plus bench.py's max-over-ranks timing reduce.
+the host gathers the hypotheses to rank 0.  The ranks here run bench.py's own
+shard plan (shard_range, uneven splits included), record packing, gather
+(gather_hypotheses over gloo), merge/count check and digest, with the CPU
+oracle standing in for each rank's decoder; plus bench.py's max-over-ranks
+timing reduce.
 """
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import ROOT, oracle
 
-T, B_PER, V, BEAM = 30, 3, 12, 6
+T, V, BEAM = 30, 12, 6
 
 
 def _free_port():
@@ -27,37 +30,80 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _decode_arrays(emis):
+    """(labels [B][T], lengths [B], logp [B]) of the best hypotheses, in the
+    array form CTCDecoder.best_arrays() hands bench.py."""
+    Tn, B, _ = emis.shape
+    best = oracle.decode(emis, BEAM, 0, max_hyps=1)
+    lab = np.zeros((B, Tn), np.int32)
+    ln = np.zeros(B, np.int32)
+    lp = np.zeros(B, np.float64)
+    for b, ((l, p),) in enumerate(best):
+        lab[b, :len(l)] = l
+        ln[b] = len(l)
+        lp[b] = p
+    return lab, ln, lp
+
+
+def _worker(rank, world, port, global_batch, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench   # bench.py: shard plan + timing reduce
-    first = bench.shard_first(rank, B_PER)
-    emis = oracle.synthetic_emissions(T, B_PER, V, first=first)
-    mine = oracle.decode(emis, BEAM, 0, max_hyps=1)
-    best = [(lab, lp) for ((lab, lp),) in mine]
-    gathered = [None] * world
-    dist.all_gather_object(gathered, best)          # host-side gather of hypotheses
+    import bench   # the product's shard plan, gather, merge and digest
+    first, count = bench.shard_range(rank, world, global_batch)
+    emis = oracle.synthetic_emissions(T, count, V, first=first)
+    lab, ln, lp = _decode_arrays(emis)
+    records = bench.gather_hypotheses(bench.pack_hypotheses(first, lab, ln, lp), world, rank)
     slowest = bench.reduce_max_over_ranks(float(rank + 1), world)
     dist.barrier()
     if rank == 0:
-        q.put(([h for part in gathered for h in part], slowest))
+        hyps, lps = bench.merge_records(records)
+        q.put((hyps, lps.tolist(), bench.hyp_digest(hyps, lps), slowest))
+    else:
+        assert records is None
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_gather_equals_single_process():
+@pytest.mark.parametrize("global_batch", [6, 7])   # even and uneven splits
+def test_two_rank_shard_gather_equals_single_process(global_batch):
+    sys.path.insert(0, str(ROOT))
+    import bench
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    import sys
-    sys.path.insert(0, str(ROOT))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, global_batch, q)) for r in range(world)]
     for p in procs:
         p.start()
-    hyps, slowest = q.get(timeout=300)
+    hyps, lps, digest, slowest = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    full = oracle.decode(oracle.synthetic_emissions(T, B_PER * world, V), BEAM, 0, max_hyps=1)
-    assert hyps == [(lab, lp) for ((lab, lp),) in full]
+    assert len(hyps) == global_batch
+    lab, ln, lp = _decode_arrays(oracle.synthetic_emissions(T, global_batch, V))
+    rec = bench.pack_hypotheses(0, lab, ln, lp)
+    assert hyps == rec[1]
+    assert lps == rec[2]
+    assert digest == bench.hyp_digest(rec[1], np.asarray(rec[2]))
     assert slowest == float(world)
+
+
+def test_shard_range_covers_batch():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    for gb in (1, 7, 64, 2048, 2049):
+        for world in (1, 2, 3, 8):
+            spans = [bench.shard_range(r, world, gb) for r in range(world)]
+            nxt = 0
+            for first, count in spans:
+                assert first == nxt and count >= 0
+                nxt += count
+            assert nxt == gb
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def test_merge_records_rejects_gaps():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    with pytest.raises(AssertionError):
+        bench.merge_records([(0, [[1]], [0.0]), (2, [[2]], [0.0])])

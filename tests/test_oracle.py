@@ -12,7 +12,7 @@ import math
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, oracle
+from conftest import GOLDEN, ROOT, oracle
 
 
 def _collapse(path, blank):
@@ -127,3 +127,15 @@ def test_threads_deterministic():
     a = oracle.decode(emis, 10, 0, nthreads=1)
     b = oracle.decode(emis, 10, 0, nthreads=4)
     assert a == b
+
+
+def test_oracle_under_sanitizers():
+    """ASan + UBSan build of the CPU restatement over its edge cases (SURVEY
+    §5 'Race detection'; oracle/sanitize_main.cpp).  Host code only."""
+    import subprocess
+    odir = ROOT / "oracle"
+    subprocess.run(["make", "-s", "-C", str(odir), "sanitize"], check=True)
+    r = subprocess.run([str(odir / "ctc_oracle_sanitize")], capture_output=True, text=True,
+                       timeout=300, env={**__import__("os").environ, "ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "oracle sanitizer run: ok" in r.stdout

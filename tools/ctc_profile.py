@@ -29,12 +29,26 @@ WPOINTS = {1: "P1 cand", 2: "folds>=G", 3: "select", 4: "fallback/cu", 7: "at of
            5: "offsets done", 8: "own prefixes", 9: "desc written", 10: "ext built", 6: "frame end"}
 
 
+def bench_emissions(T, B, V, H=256):
+    """Log-probability emissions of bench.py's model (RNN -> Linear +
+    log_softmax, random-init weights), as the headline bench decodes them."""
+    import bench
+    (w_ih, w_hh, b_ih, b_hh), (w_out, b_out) = bench.make_weights(H, H, V)
+    DM = asr.DeviceMatrix.from_numpy
+    hid, em = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, V)
+    asr.rnn_fwd(DM(bench.make_features(T, B, H, 0)), DM(w_ih), DM(w_hh), DM(b_ih.reshape(H, 1)),
+                DM(b_hh.reshape(H, 1)), hid, T, B)
+    asr.linear_fwd(hid, DM(w_out), DM(b_out.reshape(V, 1)), em, asr.EPI_BIAS_LOGSOFTMAX)
+    return em.toCpu().reshape(T, B, V)
+
+
 def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
-    emis = oracle.synthetic_emissions(T, B, V, sigma=sigma)
+    is_log = sigma == "bench"
+    emis = bench_emissions(T, B, V) if is_log else oracle.synthetic_emissions(T, B, V, sigma=sigma)
     dec = asr.CTCDecoder(V, beam, 0, waves=waves)
     ms = []
     for _ in range(reps):
-        dec.decode(emis)
+        dec.decode(emis, is_log=is_log)
         dec.best()
         ms.append(dec.last_kernel_ms())
     out = {"T": T, "B": B, "V": V, "beam": beam, "sigma": sigma, "waves": dec.config()[1],
@@ -86,15 +100,17 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--waves", default="1,2,4")
     ap.add_argument("--cases", default="c2,c3")
+    ap.add_argument("--sigmas", default="3,0.5,bench", help="synthetic emission spreads; 'bench' = bench.py's model")
     args = ap.parse_args()
-    global WAVES
+    global WAVES, SIGMAS
     WAVES = [int(x) for x in args.waves.split(",")]
+    SIGMAS = [x if x == "bench" else float(x) for x in args.sigmas.split(",")]
     asr.set_device(0)
     ap_cases = {"c2": (500, 64, 29, 50), "c3": (1000, 256, 29, 100),
                 "c5": (2000, 32, 1000, 200)}   # C5: 32 utterances per GPU
     ap_cases = [ap_cases[c] for c in args.cases.split(",")]
     for (T, B, V, beam) in ap_cases:
-        for sigma in (3.0, 0.5):
+        for sigma in SIGMAS:
             for waves in WAVES:
                 print(json.dumps(run(T, B, V, beam, sigma, waves, args.reps, args.stamps, args.wstamps)), flush=True)
 

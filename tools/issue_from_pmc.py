@@ -1,0 +1,82 @@
+"""Summarise a rocprofv3 SQ counter pass over bench.py into
+profiles/r02/issue.json: the decoder kernel's instruction-issue roofline,
+which bench.py embeds as roofline.issue.
+
+Counters (one pass, 8 SQ slots): SQ_WAVES, SQ_INSTS_VALU, SQ_INSTS_SALU,
+SQ_INSTS_LDS, SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_WAIT_INST_ANY,
+SQ_ACTIVE_INST_ANY.  Units (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* /
+SQ_ACTIVE_INST_* count quad-cycles (x4 = shader cycles); WAIT_ANY +
+WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES.
+
+Derived, per launch (one workgroup of NW waves per utterance, one workgroup
+per CU at the bench's batch, every wave alive for the whole kernel):
+  kernel_cycles  = 4 * WAVE_CYCLES / WAVES   (a wave's lifetime in cycles)
+  per wave-frame = INSTS_x / WAVES / T
+  active_frac    = ACTIVE_INST_ANY / WAVE_CYCLES  (cycles a wave issues)
+  wait_frac      = WAIT_ANY / WAVE_CYCLES         (parked: s_waitcnt / barrier)
+  stall_frac     = WAIT_INST_ANY / WAVE_CYCLES    (issue-stalled)
+  salu_util      = SALU per CU / kernel_cycles: against the CU's one scalar
+                   unit (one SALU issue per cycle)
+  valu_util      = 2 * VALU per SIMD / kernel_cycles: a wave64 VALU op holds
+                   a SIMD-32 for >= 2 cycles (fp64 and transcendental ops more)
+  lds_util       = 2 * LDS per CU / kernel_cycles: >= 2 LDS-array cycles per
+                   wave instruction (MI355X_MICROARCH.md §LDS)
+
+    python tools/issue_from_pmc.py SQ.csv --kernel ctc_beam_kernel --T 500 --B 64 \
+        --workload C2 [--source label]
+"""
+import argparse
+import csv
+import json
+from pathlib import Path
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--kernel", default="ctc_beam_kernel")
+    ap.add_argument("--T", type=int, required=True)
+    ap.add_argument("--B", type=int, required=True)
+    ap.add_argument("--workload", default="C2")
+    ap.add_argument("--source", default="")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    per = {}   # dispatch -> counter -> value
+    for r in csv.DictReader(open(args.csv)):
+        if args.kernel not in r["Kernel_Name"]:
+            continue
+        per.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    if not per:
+        raise SystemExit(f"no {args.kernel} dispatches in {args.csv}")
+    keys = sorted({k for d in per.values() for k in d})
+    avg = {k: sum(d.get(k, 0.0) for d in per.values()) / len(per) for k in keys}
+    waves = avg["SQ_WAVES"]
+    nw = waves / args.B
+    cyc = 4.0 * avg["SQ_WAVE_CYCLES"] / waves
+    wf = waves * args.T
+    issue = {
+        "dispatches": len(per),
+        "waves_per_workgroup": round(nw, 2),
+        "kernel_cycles": round(cyc),
+        "cycles_per_frame": round(cyc / args.T, 1),
+        "valu_per_wave_frame": round(avg["SQ_INSTS_VALU"] / wf, 1),
+        "salu_per_wave_frame": round(avg["SQ_INSTS_SALU"] / wf, 1),
+        "lds_per_wave_frame": round(avg["SQ_INSTS_LDS"] / wf, 1),
+        "active_frac": round(avg["SQ_ACTIVE_INST_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
+        "wait_frac": round(avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
+        "stall_frac": round(avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
+        "salu_util": round(avg["SQ_INSTS_SALU"] / args.B / cyc, 4),
+        "valu_util": round(2.0 * avg["SQ_INSTS_VALU"] / (4 * args.B) / cyc, 4),
+        "lds_util": round(2.0 * avg["SQ_INSTS_LDS"] / args.B / cyc, 4),
+    }
+    out = {"workload": args.workload, "kernel": args.kernel, "T": args.T, "B": args.B,
+           "counters_avg_per_launch": {k: round(v) for k, v in avg.items()},
+           "issue": issue, "source": args.source}
+    p = Path(args.out) if args.out else Path(__file__).resolve().parents[1] / "profiles" / "r02" / "issue.json"
+    p.parent.mkdir(parents=True, exist_ok=True)
+    p.write_text(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
