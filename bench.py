@@ -176,13 +176,14 @@ def load_profile_json(name: str):
         return None
 
 
-def load_traffic(kernel: str):
-    """Measured HBM bytes per launch of `kernel` (rocprofv3 FETCH_SIZE +
-    WRITE_SIZE passes, summarised by tools/traffic_from_pmc.py into the
-    committed profiles/traffic.json); None when not profiled."""
-    d = load_profile_json("traffic.json")
+def load_traffic(kernel: str, workload: str):
+    """Measured HBM bytes per launch of `kernel` at `workload` (rocprofv3
+    FETCH_SIZE + WRITE_SIZE passes over this bench at that configuration,
+    summarised by tools/traffic_from_pmc.py into the committed
+    profiles/r02/traffic.json); None when that workload was not profiled."""
+    d = load_profile_json("r02/traffic.json")
     try:
-        return d[kernel]["hbm_bytes_per_launch"]
+        return d[workload][kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -405,7 +406,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "avg_launch_ms": round(avg_kernel_ms, 4), "bytes_per_frame": bpf,
                 "frames_per_launch": B * T, "us_per_frame_step": round(1e3 * avg_kernel_ms / T, 4),
-                "traffic": load_traffic(kname),
+                "traffic": load_traffic(kname, args.config if not args.decode_only else None),
                 "limiter": "on-chip issue/latency (beam resident in LDS; HBM traffic is ~8 MB per "
                            "launch): see roofline.issue"}
         iss = load_profile_json("r02/issue.json")

@@ -16,51 +16,70 @@ namespace asr {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 64;   // rows per workgroup: 4 waves x 16 rows
-constexpr int BK = 16;   // k per LDS stage
-constexpr int AST = BK + 2;   // As row stride (floats): conflict-free A-fragment reads
 
-template <int BN>
+// One K stage of a 64 x BN tile in LDS.  As row stride BK + 2: the A-fragment
+// reads of a half-wave (16 rows x 2 k) land in distinct banks; Bs row stride
+// BN + 16: k and k+1 land 16 banks apart.
+template <int BN, int BK>
 struct Tile {
-    static constexpr int BST = BN + 16;   // Bs row stride: k and k+1 land 16 banks apart
+    static constexpr int AST = BK + 2;
+    static constexpr int BST = BN + 16;
     float As[BM * AST];
     float Bs[BK * BST];
 };
 
 // Accumulate A[M,K] . B[K,N] for this workgroup's 64 x BN tile into acc[].
-// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn].  VEC: sak == 1 and
-// sbn == 1 with 16-byte aligned rows, loaded as float4.
-template <int BN, bool VEC>
-__device__ __forceinline__ void mma_tile(Tile<BN>& L, const float* __restrict__ A,
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn].  VEC bit 0: A rows
+// contiguous and 16-byte aligned (sak == 1, K and sam multiples of 4), loaded
+// as float4; bit 1: the same for B rows (sbn == 1, N and sbk multiples of 4).
+// The two are independent so that a narrow N (the emission projection's
+// V = 29) still streams the wide A operand (the hiddens) as float4.
+// BK = 64 keeps 16 KB of A per workgroup in flight per stage (the emission
+// projection is a latency-bound stream at BK = 16: one 4 KB stage per round
+// trip); the next stage is loaded into registers during the MFMAs.
+template <int BN, int BK, int VEC>
+__device__ __forceinline__ void mma_tile(Tile<BN, BK>& L, const float* __restrict__ A,
                                          const float* __restrict__ Bm, int M, int N, int K,
                                          long sam, long sak, long sbk, long sbn, int m0, int n0,
                                          f32x4 (&acc)[BN / 16]) {
-    constexpr int BST = Tile<BN>::BST;
-    constexpr int NB4 = BN / 4;                 // float4 per B row
+    constexpr int AST = Tile<BN, BK>::AST, BST = Tile<BN, BK>::BST;
+    constexpr int KA4 = BK / 4;                  // float4 per A row of a stage
+    constexpr int NA = BM * KA4 / 256;           // A float4 per thread (BK >= 16)
+    constexpr int NB4 = BN / 4;                  // float4 per B row
+    constexpr int BTOT = BK * NB4;               // B float4 per stage
+    constexpr int NB = (BTOT + 255) / 256;       // B float4 per thread (some idle when BTOT < 256)
+    static_assert(NA >= 1 && BM * KA4 == NA * 256, "A stage split");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int ar = tid >> 2, ak = (tid & 3) * 4;            // A: 64 rows x 4 float4
-    const int bkr = tid / NB4, bn = (tid % NB4) * 4;        // B: 16 rows x NB4 float4
-    const bool bact = tid < BK * NB4;
-    float ra[4], rb[4];
+    float ra[NA][4], rb[NB][4];
 
     auto load = [&](int k0) {
-        const int gm = m0 + ar, gk = k0 + ak;
-        if (VEC && gm < M && gk + 3 < K) {
-            const float4 v = *reinterpret_cast<const float4*>(A + gm * sam + gk);
-            ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
-        } else {
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                ra[i] = (gm < M && gk + i < K) ? A[gm * sam + (long)(gk + i) * sak] : 0.f;
-        }
-        const int gkb = k0 + bkr, gn = n0 + bn;
-        if (bact) {
-            if (VEC && gkb < K && gn + 3 < N) {
-                const float4 v = *reinterpret_cast<const float4*>(Bm + gkb * sbk + gn);
-                rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
+        for (int i = 0; i < NA; i++) {
+            const int idx = tid + 256 * i;
+            const int ar = idx / KA4, ak = (idx % KA4) * 4;
+            const int gm = m0 + ar, gk = k0 + ak;
+            if ((VEC & 1) && gm < M && gk + 3 < K) {
+                const float4 v = *reinterpret_cast<const float4*>(A + gm * sam + gk);
+                ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
             } else {
 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    rb[i] = (gkb < K && gn + i < N) ? Bm[gkb * sbk + (long)(gn + i) * sbn] : 0.f;
+                for (int e = 0; e < 4; e++)
+                    ra[i][e] = (gm < M && gk + e < K) ? A[gm * sam + (long)(gk + e) * sak] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            const int idx = tid + 256 * i;
+            if (idx >= BTOT) continue;
+            const int bkr = idx / NB4, bn = (idx % NB4) * 4;
+            const int gkb = k0 + bkr, gn = n0 + bn;
+            if ((VEC & 2) && gkb < K && gn + 3 < N) {
+                const float4 v = *reinterpret_cast<const float4*>(Bm + gkb * sbk + gn);
+                rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    rb[i][e] = (gkb < K && gn + e < N) ? Bm[gkb * sbk + (long)(gn + e) * sbn] : 0.f;
             }
         }
     };
@@ -69,10 +88,19 @@ __device__ __forceinline__ void mma_tile(Tile<BN>& L, const float* __restrict__ 
     for (int k0 = 0; k0 < K; k0 += BK) {
         __syncthreads();   // previous stage fully consumed
 #pragma unroll
-        for (int i = 0; i < 4; i++) L.As[ar * AST + ak + i] = ra[i];
-        if (bact) {
+        for (int i = 0; i < NA; i++) {
+            const int idx = tid + 256 * i;
+            const int ar = idx / KA4, ak = (idx % KA4) * 4;
 #pragma unroll
-            for (int i = 0; i < 4; i++) L.Bs[bkr * BST + bn + i] = rb[i];
+            for (int e = 0; e < 4; e++) L.As[ar * AST + ak + e] = ra[i][e];
+        }
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            const int idx = tid + 256 * i;
+            if (idx >= BTOT) continue;
+            const int bkr = idx / NB4, bn = (idx % NB4) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; e++) L.Bs[bkr * BST + bn + e] = rb[i][e];
         }
         __syncthreads();
         if (k0 + BK < K) load(k0 + BK);   // next stage in flight during the MFMAs
@@ -90,9 +118,9 @@ __device__ __forceinline__ void mma_tile(Tile<BN>& L, const float* __restrict__ 
 
 // C/D layout of 16x16 MFMA tiles (dtype-independent on gfx950):
 // element j of lane l is row (l>>4)*4 + j, column l & 15.
-template <int BN, int EPI, bool VEC>
+template <int BN, int BK, int EPI, int VEC>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
-    __shared__ Tile<BN> L;
+    __shared__ Tile<BN, BK> L;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     f32x4 acc[BN / 16], acc2[BN / 16];
@@ -101,9 +129,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         acc2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    mma_tile<BN, VEC>(L, g.A, g.B, g.M, g.N, g.K, g.sam, g.sak, g.sbk, g.sbn, m0, n0, acc);
+    mma_tile<BN, BK, VEC>(L, g.A, g.B, g.M, g.N, g.K, g.sam, g.sak, g.sbk, g.sbn, m0, n0, acc);
     if (EPI == EPI_DUAL_TANH)
-        mma_tile<BN, VEC>(L, g.A2, g.B2, g.M, g.N, g.K2, g.K2, 1, g.N, 1, m0, n0, acc2);
+        mma_tile<BN, BK, VEC>(L, g.A2, g.B2, g.M, g.N, g.K2, g.K2, 1, g.N, 1, m0, n0, acc2);
 
     const int rbase = m0 + w * 16 + (lane >> 4) * 4;
     if (EPI == EPI_LOGSOFTMAX) {
@@ -162,17 +190,30 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     }
 }
 
-template <int BN, int EPI>
-static int launch_gemm_bn(const GemmArgs& g, hipStream_t s) {
+template <int BN, int BK, int EPI>
+static int launch_gemm_bk(const GemmArgs& g, hipStream_t s) {
     const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
-    bool vec = g.sak == 1 && g.sbn == 1 && (g.K % 4) == 0 && (g.N % 4) == 0 &&
-               ((uintptr_t)g.A % 16) == 0 && ((uintptr_t)g.B % 16) == 0;
-    if (EPI == EPI_DUAL_TANH)
-        vec = vec && (g.K2 % 4) == 0 && ((uintptr_t)g.A2 % 16) == 0 && ((uintptr_t)g.B2 % 16) == 0;
-    if (vec) hipLaunchKernelGGL((gemm_kernel<BN, EPI, true>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_kernel<BN, EPI, false>), grid, dim3(256), 0, s, g);
+    bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
+    bool vb = g.sbn == 1 && (g.N % 4) == 0 && (g.sbk % 4) == 0 && ((uintptr_t)g.B % 16) == 0;
+    if (EPI == EPI_DUAL_TANH) {   // second operand pair: A2 [M][K2], B2 [K2][N]
+        va = va && (g.K2 % 4) == 0 && ((uintptr_t)g.A2 % 16) == 0;
+        vb = vb && ((uintptr_t)g.B2 % 16) == 0;
+    }
+    const int vec = (va ? 1 : 0) | (vb ? 2 : 0);
+    if (vec == 3) hipLaunchKernelGGL((gemm_kernel<BN, BK, EPI, 3>), grid, dim3(256), 0, s, g);
+    else if (vec == 1) hipLaunchKernelGGL((gemm_kernel<BN, BK, EPI, 1>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_kernel<BN, BK, EPI, 0>), grid, dim3(256), 0, s, g);
     ASR_LAUNCH_TRY();
     return ASR_OK;
+}
+
+// 64-deep K stages once K is long enough to fill them (both operand pairs
+// for the dual GEMM), 16-deep otherwise.
+template <int BN, int EPI>
+static int launch_gemm_bn(const GemmArgs& g, hipStream_t s) {
+    const int kmin = EPI == EPI_DUAL_TANH ? (g.K < g.K2 ? g.K : g.K2) : g.K;
+    if (kmin >= 128) return launch_gemm_bk<BN, 64, EPI>(g, s);
+    return launch_gemm_bk<BN, 16, EPI>(g, s);
 }
 
 template <int EPI>

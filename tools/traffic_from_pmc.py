@@ -1,5 +1,7 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/traffic.json
-(HBM bytes per launch of each kernel), which bench.py embeds as roofline.traffic.
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into
+profiles/r02/traffic.json (HBM bytes per launch of each kernel, keyed by the
+bench workload the passes ran), which bench.py embeds as roofline.traffic for
+that workload only.
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md:
 FETCH_SIZE reads exactly half the bytes of 16-B/lane coalesced streaming
@@ -7,7 +9,7 @@ reads; the decoder's emission loads are 4-B/lane global_load_dword, for
 which the counter is not halved (checked: 4055 KiB vs 3.71 MB of emission
 rows per C2 launch), so no correction is applied to the decoder.
 
-    python tools/traffic_from_pmc.py FETCH.csv WRITE.csv [source-label]
+    python tools/traffic_from_pmc.py FETCH.csv WRITE.csv WORKLOAD [source-label]
 """
 import csv
 import json
@@ -27,13 +29,16 @@ def per_kernel(path):
 
 def main():
     fetch, write = per_kernel(sys.argv[1]), per_kernel(sys.argv[2])
-    label = sys.argv[3] if len(sys.argv) > 3 else ""
+    workload = sys.argv[3]
+    label = sys.argv[4] if len(sys.argv) > 4 else ""
+    p = Path(__file__).resolve().parents[1] / "profiles" / "r02" / "traffic.json"
+    allw = json.loads(p.read_text()) if p.exists() else {}
     out = {}
     for k in sorted(set(fetch) & set(write)):
         out[k] = {"fetch_kib": round(fetch[k], 1), "write_kib": round(write[k], 1),
                   "hbm_bytes_per_launch": int((fetch[k] + write[k]) * 1024), "source": label}
-    p = Path(__file__).resolve().parents[1] / "profiles" / "traffic.json"
-    p.write_text(json.dumps(out, indent=1))
+    allw[workload] = out
+    p.write_text(json.dumps(allw, indent=1))
     print(json.dumps(out, indent=1))
 
 
