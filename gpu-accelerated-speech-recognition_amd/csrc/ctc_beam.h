@@ -5,7 +5,7 @@
 namespace asr {
 
 #ifdef ASR_CTC_WSTAMPS
-constexpr int NSTAMP = 16 * 8;   // diagnostic: per-wave arrival clocks per utterance
+constexpr int NSTAMP = 16 * 9;   // diagnostic: per-wave arrival clocks per utterance + critical path
 #else
 constexpr int NSTAMP = 16;   // diagnostic phase clocks per utterance
 #endif

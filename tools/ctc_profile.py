@@ -57,7 +57,7 @@ def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
     if wstamps:   # per-wave arrival clocks (libasr_amd_wstamps.so)
         L = asr.lib()
         nw = dec.config()[1]
-        buf = np.zeros((B, 8, 16), np.uint64)
+        buf = np.zeros((B, 9, 16), np.uint64)
         fn = L.asr_debug_ctc_stamps
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         asr.check(fn(dec.h, buf.ctypes.data), "stamps")
@@ -65,6 +65,10 @@ def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
         per = buf[:, :nw, :].astype(np.float64).sum(axis=0) / frames[:, None]
         order = sorted(WPOINTS, key=lambda i: per[0, i])
         out["arrival_cycles_by_wave"] = {WPOINTS[i]: [round(x) for x in per[:, i]] for i in order}
+        # critical path: per frame, the last wave's arrival at each point
+        # (relative to wave 0's frame start), averaged over frames
+        crit = buf[:, 8, :].astype(np.float64).sum(axis=0) / max(1.0, buf[:, 8, 0].astype(np.float64).sum())
+        out["last_wave_arrival"] = {WPOINTS[i]: round(crit[i]) for i in sorted(WPOINTS, key=lambda i: crit[i])}
     if stamps and dec.config()[1] == 0:   # one-wave list kernel: phase clocks and counters
         L = asr.lib()
         buf = np.zeros((B, 16), np.uint64)
