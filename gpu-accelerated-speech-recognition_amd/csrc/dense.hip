@@ -207,12 +207,16 @@ static int launch_gemm_bk(const GemmArgs& g, hipStream_t s) {
     return ASR_OK;
 }
 
-// 64-deep K stages once K is long enough to fill them (both operand pairs
-// for the dual GEMM), 16-deep otherwise.
+// 64-deep K stages for narrow outputs (the emission projection, N = V <= 32:
+// a latency-bound stream of A; measured 27.4 -> 17.2 us at C2), 16-deep
+// otherwise (wide N is MFMA-bound and keeps more workgroups per CU with the
+// smaller LDS tile: the C2 input projection ran 52.8 us at BK 16, 68.0 at 64).
 template <int BN, int EPI>
 static int launch_gemm_bn(const GemmArgs& g, hipStream_t s) {
     const int kmin = EPI == EPI_DUAL_TANH ? (g.K < g.K2 ? g.K : g.K2) : g.K;
-    if (kmin >= 128) return launch_gemm_bk<BN, 64, EPI>(g, s);
+    if constexpr (BN == 32) {
+        if (kmin >= 128) return launch_gemm_bk<BN, 64, EPI>(g, s);
+    }
     return launch_gemm_bk<BN, 16, EPI>(g, s);
 }
 
