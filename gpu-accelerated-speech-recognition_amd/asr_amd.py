@@ -39,6 +39,7 @@ ASR_ERR_INTERNAL = 7
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_LOGSOFTMAX = 0, 1, 2, 3
 SEMANTICS_CPU, SEMANTICS_CUDA = 0, 1   # asr_ctc_set_semantics
+ASR_CTC_WAVES_LIST = -1                # asr_ctc_set_waves: the one-wave list kernel
 
 # Every symbol include/asr_amd.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
@@ -51,6 +52,7 @@ EXPORTS = [
     "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
+    "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts",
 ]
 
 
@@ -113,6 +115,8 @@ def lib() -> ctypes.CDLL:
         "asr_ctc_get_config": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_ctc_decode_ex": [_vp, _vp, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
         "asr_ctc_set_semantics": [_vp, _i],
+        "asr_ctc_set_timesteps": [_vp, _i],
+        "asr_ctc_get_beams_ts": [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -335,6 +339,10 @@ class CTCDecoder:
         (CTCBeamSearch.cu: exactly beam states, strip-then-merge last step)."""
         check(lib().asr_ctc_set_semantics(self.h, semantics), "asr_ctc_set_semantics")
 
+    def set_timesteps(self, on: bool) -> None:
+        """Record each label's append frame in later decodes (beams_ts)."""
+        check(lib().asr_ctc_set_timesteps(self.h, int(bool(on))), "asr_ctc_set_timesteps")
+
     def decode_device(self, d_emis: int, T: int, B: int, is_log: bool, stream: int = 0,
                       lengths: Optional[Sequence[int]] = None, frame_stride: Optional[int] = None,
                       utt_stride: Optional[int] = None) -> None:
@@ -398,6 +406,20 @@ class CTCDecoder:
         return [[(lab[b, k, :ln[b, k]].tolist(), float(lp[b, k])) for k in range(min(nh[b], max_hyps))]
                 for b in range(B)]
 
+    def beams_ts(self, max_hyps: int) -> List[List[Tuple[List[int], float, List[int]]]]:
+        """Ranked final beam with each label's append frame: [(labels, logp,
+        timesteps)] per utterance (timesteps mode must have been on)."""
+        B, T = self.B, self.T
+        nh = np.zeros(B, np.int32)
+        ln = np.zeros((B, max_hyps), np.int32)
+        lab = np.zeros((B, max_hyps, max(T, 1)), np.int32)
+        lp = np.zeros((B, max_hyps), np.float64)
+        ts = np.zeros((B, max_hyps, max(T, 1)), np.int32)
+        check(lib().asr_ctc_get_beams_ts(self.h, max_hyps, max(T, 1), _ptr(nh), _ptr(ln), _ptr(lab),
+                                         _ptr(lp), _ptr(ts)), "asr_ctc_get_beams_ts")
+        return [[(lab[b, k, :ln[b, k]].tolist(), float(lp[b, k]), ts[b, k, :ln[b, k]].tolist())
+                 for k in range(min(nh[b], max_hyps))] for b in range(B)]
+
     def last_kernel_ms(self) -> float:
         ms = _f()
         check(lib().asr_ctc_last_kernel_ms(self.h, ctypes.byref(ms)), "asr_ctc_last_kernel_ms")
@@ -450,10 +472,14 @@ class CTCBeamDecoder:
     F1-F3), not ctcdecode's; no language model (model_path must
     be None).  decode returns (beam_results [B, beam_width, T] int32 label
     ids, beam_scores [B, beam_width] float32 = -log p (lower is better),
-    timesteps [B, beam_width, T] int32 = -1 (not tracked), out_lens
-    [B, beam_width] int32); hypotheses beyond an utterance's final beam have
-    length 0 and score +inf.  probs may be a numpy array or a torch tensor
-    (a GPU tensor is decoded in place, no copy)."""
+    timesteps [B, beam_width, T] int32, out_lens [B, beam_width] int32);
+    hypotheses beyond an utterance's final beam have length 0 and score +inf.
+    timesteps[b, k, i] is the frame at which label i of hypothesis k was
+    appended in the surviving search lineage (asr_ctc_set_timesteps; ctcdecode
+    reports the frame of its trie node's best emission, so the two agree in
+    meaning but are not pinned against each other: ctcdecode is unavailable
+    here); -1 past a hypothesis' length.  probs may be a numpy array or a
+    torch tensor (a GPU tensor is decoded in place, no copy)."""
 
     def __init__(self, labels: Sequence[str], model_path: Optional[str] = None, alpha: float = 0.0,
                  beta: float = 0.0, cutoff_top_n: int = 40, cutoff_prob: float = 1.0,
@@ -464,6 +490,7 @@ class CTCBeamDecoder:
         self.labels = list(labels)
         self.beam_width, self.blank_id, self.log_probs_input = beam_width, blank_id, log_probs_input
         self._dec = CTCDecoder(len(self.labels), beam_width, blank_id)
+        self._dec.set_timesteps(True)
 
     def decode(self, probs, seq_lens=None):
         B, T, V = (int(x) for x in probs.shape)
@@ -481,13 +508,15 @@ class CTCBeamDecoder:
             arr = probs.cpu().numpy() if hasattr(probs, "cpu") else np.asarray(probs)
             self._dec.decode(arr, is_log=self.log_probs_input, lengths=lens, batch_major=True)
         K = self.beam_width
-        beams = self._dec.beams(max_hyps=self._dec.config()[0])
+        beams = self._dec.beams_ts(max_hyps=self._dec.config()[0])
         results = np.zeros((B, K, T), np.int32)
         scores = np.full((B, K), np.inf, np.float32)
+        timesteps = np.full((B, K, T), -1, np.int32)
         out_lens = np.zeros((B, K), np.int32)
         for b, hyps in enumerate(beams):
-            for k, (lab, lp) in enumerate(hyps[:K]):
+            for k, (lab, lp, ts) in enumerate(hyps[:K]):
                 results[b, k, :len(lab)] = lab
                 scores[b, k] = -lp
+                timesteps[b, k, :len(ts)] = ts
                 out_lens[b, k] = len(lab)
-        return results, scores, np.full((B, K, T), -1, np.int32), out_lens
+        return results, scores, timesteps, out_lens

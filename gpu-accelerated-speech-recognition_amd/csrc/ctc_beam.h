@@ -33,6 +33,8 @@ struct CtcArgs {
     uint64_t blank_less;    // bit c: code(blank) < code(c)   (V <= 64 kernels)
     const int* codes;       // [V] symbol codes (device; wide-vocabulary kernel)
     int4* nodes;            // [B][T*kcap] (parent node, 0, 8 labels packed lo, hi)
+    int4* nodes_ts;         // [B][T*kcap] append frames of a record's labels, 16 bits each (NULL: no timesteps)
+    uint64_t* fin_ts;       // [B][kcap][2] append frames of the final tails' labels (timesteps mode)
     int* fin_n;             // [B] final hypotheses
     int* fin_node;          // [B][kcap]
     uint64_t* fin_tail;     // [B][kcap]  labels after fin_node's block (count << 56)
@@ -64,7 +66,7 @@ int ctc_set_max_lds_wave();
 // waves < 0: the one-wave list kernel; 1..8: the workgroup kernel with that many waves.
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s);
-int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s);
+int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, int* d_all_ts, hipStream_t s);
 int ctc_set_max_lds();
 
 }  // namespace asr

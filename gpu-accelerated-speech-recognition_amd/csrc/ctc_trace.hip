@@ -30,6 +30,13 @@ __device__ __forceinline__ uint32_t tail_label(uint64_t tail, int k, int lbits) 
     return (uint32_t)(tail >> (lbits * k)) & ((1u << lbits) - 1u);
 }
 
+// Append frame k (16-bit field k) of a 128-bit frame record: a node's
+// nodes_ts entry, or a final tail's two fin_ts words.
+__device__ __forceinline__ int frame_field(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int k) {
+    const uint32_t wd = k < 2 ? w0 : (k < 4 ? w1 : (k < 6 ? w2 : w3));
+    return (int)((wd >> (16 * (k & 1))) & 0xFFFFu);
+}
+
 // Chase the block chain of `x` into ids[] (last block first); returns the
 // number of blocks.
 __device__ int chase_blocks(const int4* nodes, int nmax, int x, int* ids, int maxb) {
@@ -127,9 +134,10 @@ __global__ __launch_bounds__(64) void ctc_best_kernel(CtcArgs a, const int* code
 }
 
 // Full-beam traceback: every final hypothesis of every utterance, labels in
-// forward order into all_lab[b][slot][T].  One lane per hypothesis: count
-// the blocks, then chase again writing each block at its final position.
-__global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, int* all_len) {
+// forward order into all_lab[b][slot][T] (and, in timesteps mode, each
+// label's append frame into all_ts[b][slot][T]).  One lane per hypothesis:
+// count the blocks, then chase again writing each block at its final position.
+__global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, int* all_len, int* all_ts) {
     const int b = blockIdx.x;
     const int kcap = a.g.kcap;
     const int n = a.fin_n[b];
@@ -146,14 +154,30 @@ __global__ __launch_bounds__(64) void ctc_all_kernel(CtcArgs a, int* all_lab, in
         const uint64_t tail = ft[i];
         const int nt = (int)(tail >> 56) < per ? (int)(tail >> 56) : per - 1;
         const int len = per * nb + nt <= a.T ? per * nb + nt : a.T;
+        const bool ts = all_ts && a.nodes_ts;
+        int* ots = ts ? all_ts + ((size_t)b * kcap + i) * a.T : nullptr;
+        const int4* nts = ts ? a.nodes_ts + (size_t)b * a.T * kcap : nullptr;
         int j = nb - 1;
         for (int x = fn[i]; x >= 0 && x < nmax && j >= 0; x = nodes[x].x, j--) {
             const int4 r = nodes[x];
             for (int k = 0; k < per; k++)
                 if (per * j + k < len) out[per * j + k] = (int)block_label(r, k, lbits);
+            if (ts) {
+                const int4 f = nts[x];
+                for (int k = 0; k < per; k++)
+                    if (per * j + k < len)
+                        ots[per * j + k] = frame_field((uint32_t)f.x, (uint32_t)f.y, (uint32_t)f.z, (uint32_t)f.w, k);
+            }
         }
         for (int k = 0; k < nt; k++)
             if (per * nb + k < len) out[per * nb + k] = (int)tail_label(tail, k, lbits);
+        if (ts) {
+            const uint64_t f0 = a.fin_ts[((size_t)b * kcap + i) * 2], f1 = a.fin_ts[((size_t)b * kcap + i) * 2 + 1];
+            for (int k = 0; k < nt; k++)
+                if (per * nb + k < len)
+                    ots[per * nb + k] = frame_field((uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1,
+                                                    (uint32_t)(f1 >> 32), k);
+        }
         all_len[(size_t)b * kcap + i] = len;
     }
 }
@@ -174,8 +198,8 @@ int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStrea
     return ASR_OK;
 }
 
-int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, hipStream_t s) {
-    hipLaunchKernelGGL(ctc_all_kernel, dim3(a.B), dim3(64), 0, s, a, d_all_lab, d_all_len);
+int ctc_launch_all(const CtcArgs& a, int* d_all_lab, int* d_all_len, int* d_all_ts, hipStream_t s) {
+    hipLaunchKernelGGL(ctc_all_kernel, dim3(a.B), dim3(64), 0, s, a, d_all_lab, d_all_len, d_all_ts);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

@@ -295,7 +295,10 @@ struct asr_ctc {
     int *d_best_lab = nullptr, *d_best_len = nullptr;
     double* d_best_score = nullptr;
     int* d_codes = nullptr;
-    int *d_all_lab = nullptr, *d_all_len = nullptr;
+    int *d_all_lab = nullptr, *d_all_len = nullptr, *d_all_ts = nullptr;
+    int ts = 0;                      // timesteps mode (asr_ctc_set_timesteps)
+    int4* d_nodes_ts = nullptr;      // [B][T*kcap] append frames per node record
+    uint64_t* d_fin_ts = nullptr;    // [B][kcap][2] append frames of the final tails
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
     unsigned char* h_res = nullptr;   // pinned mirror of d_res
@@ -360,6 +363,8 @@ void free_ws(asr_ctc* h) {
     hipFree(h->d_fin_tail); hipFree(h->d_chain);
     h->d_fin_tail = nullptr; h->d_chain = nullptr;
     hipFree(h->d_fin_score); hipFree(h->d_res);
+    hipFree(h->d_nodes_ts); hipFree(h->d_fin_ts);
+    h->d_nodes_ts = nullptr; h->d_fin_ts = nullptr;
     hipHostFree(h->h_res);
     h->d_res = nullptr; h->h_res = nullptr;
     h->d_nodes = nullptr; h->d_fin_n = h->d_fin_node = h->d_status = nullptr;
@@ -369,7 +374,14 @@ void free_ws(asr_ctc* h) {
 }
 
 int ensure_ws(asr_ctc* h, int B, int T) {
-    if (B <= h->capB && T <= h->capT) return ASR_OK;
+    if (B <= h->capB && T <= h->capT) {
+        if (h->ts && !h->d_nodes_ts) {   // timesteps switched on after the workspace was sized
+            const size_t kc = (size_t)h->kcap;
+            ASR_HIP_TRY(hipMalloc(&h->d_nodes_ts, sizeof(int4) * (size_t)h->capB * h->capT * kc));
+            ASR_HIP_TRY(hipMalloc(&h->d_fin_ts, sizeof(uint64_t) * 2 * (size_t)h->capB * kc));
+        }
+        return ASR_OK;
+    }
     // Grow geometrically in B and T so that repeated decodes do not thrash.
     const int nB = std::max(B, h->capB), nT = std::max(T, h->capT);
     hipDeviceSynchronize();
@@ -384,6 +396,10 @@ int ensure_ws(asr_ctc* h, int B, int T) {
     const size_t res_bytes = 16 * (size_t)nB + sizeof(int) * (size_t)nB * nT;
     ASR_HIP_TRY(hipMalloc(&h->d_res, res_bytes));
     ASR_HIP_TRY(hipHostMalloc((void**)&h->h_res, res_bytes, 0));
+    if (h->ts) {
+        ASR_HIP_TRY(hipMalloc(&h->d_nodes_ts, sizeof(int4) * (size_t)nB * nT * kc));
+        ASR_HIP_TRY(hipMalloc(&h->d_fin_ts, sizeof(uint64_t) * 2 * (size_t)nB * kc));
+    }
     h->capB = nB;
     h->capT = nT;
     return ASR_OK;
@@ -465,6 +481,7 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     hipHostFree(h->h_lengths);
     hipFree(h->d_all_lab);
     hipFree(h->d_all_len);
+    hipFree(h->d_all_ts);
     hipFree(h->d_stamps);
     if (h->wide) asr_ctc_destroy(h->wide);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -480,6 +497,14 @@ int asr_ctc_set_semantics(asr_ctc_t* h, int semantics) {
     if (semantics == ASR_CTC_SEMANTICS_CUDA && h->V + 1 > 64) return ASR_ERR_UNSUPPORTED;
     h->cu_mode = semantics == ASR_CTC_SEMANTICS_CUDA ? 1 : 0;
     h->K = h->cu_mode ? h->beam : h->beam + 1;   // exactly beam states vs beam+1 and ties
+    h->have = false;
+    return ASR_OK;
+}
+
+int asr_ctc_set_timesteps(asr_ctc_t* h, int on) {
+    if (!h) return ASR_ERR_ARG;
+    h->ts = on ? 1 : 0;
+    if (h->wide) h->wide->ts = h->ts;
     h->have = false;
     return ASR_OK;
 }
@@ -530,9 +555,10 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
         std::memcpy(h->h_lengths, h_lengths, sizeof(int) * B);
         ASR_HIP_TRY(hipMemcpyAsync(h->d_lengths, h->h_lengths, sizeof(int) * B, hipMemcpyHostToDevice, st0));
     }
-    // .cu-semantics kernels exist for the automatic wave count only
-    const int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override
-                                                                       : auto_waves(h));
+    // .cu-semantics kernels exist for the automatic wave count only; the
+    // one-wave list kernel does not track timesteps
+    int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h));
+    if (h->ts && waves < 0) waves = valid_waves(h, 8);
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
@@ -550,6 +576,8 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.fin_node = h->d_fin_node;
     a.fin_tail = h->d_fin_tail;
     a.fin_score = h->d_fin_score;
+    a.nodes_ts = h->ts ? h->d_nodes_ts : nullptr;
+    a.fin_ts = h->ts ? h->d_fin_ts : nullptr;
     // packed result layout for this (B, T)
     h->d_best_score = reinterpret_cast<double*>(h->d_res);
     h->d_best_len = reinterpret_cast<int*>(h->d_res + 8 * (size_t)B);
@@ -615,6 +643,7 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
             h->wide->auto_cap = true;
             h->wide->cu_mode = h->cu_mode;
             h->wide->K = h->K;
+            h->wide->ts = h->ts;
         }
         int rc = asr_ctc_decode_ex(h->wide, h->last_emis, T, B, h->last_tstride, h->last_ustride,
                                    h->last_lengths.empty() ? nullptr : h->last_lengths.data(),
@@ -637,7 +666,13 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
 
 int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, int32_t* lengths,
                       int32_t* labels, double* logp) {
+    return asr_ctc_get_beams_ts(h, max_hyps, max_len, n_hyps, lengths, labels, logp, nullptr);
+}
+
+int asr_ctc_get_beams_ts(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, int32_t* lengths,
+                         int32_t* labels, double* logp, int32_t* timesteps) {
     if (!h || max_hyps < 1 || max_len < 0) return ASR_ERR_ARG;
+    if (timesteps && !h->ts) return ASR_ERR_STATE;   // the decode did not track them
     if (!h->have) return ASR_ERR_STATE;
     const int B = h->lastB, T = h->lastT, kc = h->kcap;
     const hipStream_t st = h->stream;
@@ -646,21 +681,25 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
         hipStreamSynchronize(st);
         hipFree(h->d_all_lab);
         hipFree(h->d_all_len);
-        h->d_all_lab = nullptr; h->d_all_len = nullptr; h->cap_all = 0;
+        hipFree(h->d_all_ts);
+        h->d_all_lab = nullptr; h->d_all_len = nullptr; h->d_all_ts = nullptr; h->cap_all = 0;
         ASR_HIP_TRY(hipMalloc(&h->d_all_lab, sizeof(int) * need));
         ASR_HIP_TRY(hipMalloc(&h->d_all_len, sizeof(int) * (size_t)B * kc));
         h->cap_all = need;
     }
-    int rc = asr::ctc_launch_all(h->args, h->d_all_lab, h->d_all_len, st);
+    if (timesteps && !h->d_all_ts) ASR_HIP_TRY(hipMalloc(&h->d_all_ts, sizeof(int) * h->cap_all));
+    int rc = asr::ctc_launch_all(h->args, h->d_all_lab, h->d_all_len, timesteps ? h->d_all_ts : nullptr, st);
     if (rc) return rc;
     std::vector<int> fin_n(B), all_len((size_t)B * kc), status(B);
     std::vector<double> score((size_t)B * kc);
-    std::vector<int> lab(need);
+    std::vector<int> lab(need), tsv(timesteps ? need : 0);
     ASR_HIP_TRY(hipMemcpyAsync(fin_n.data(), h->d_fin_n, sizeof(int) * B, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(status.data(), h->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(score.data(), h->d_fin_score, sizeof(double) * B * kc, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(all_len.data(), h->d_all_len, sizeof(int) * B * kc, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(lab.data(), h->d_all_lab, sizeof(int) * need, hipMemcpyDeviceToHost, st));
+    if (timesteps)
+        ASR_HIP_TRY(hipMemcpyAsync(tsv.data(), h->d_all_ts, sizeof(int) * need, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipStreamSynchronize(st));
     const int stc = status_code(status.data(), B);
     if (stc == ASR_ERR_BEAM_OVERFLOW && h->auto_cap && h->kcap < 256) {
@@ -671,12 +710,13 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
             h->wide->auto_cap = true;
             h->wide->cu_mode = h->cu_mode;
             h->wide->K = h->K;   // keeps doubling, up to 256 states
+            h->wide->ts = h->ts;
         }
         rc = asr_ctc_decode_ex(h->wide, h->last_emis, T, B, h->last_tstride, h->last_ustride,
                                h->last_lengths.empty() ? nullptr : h->last_lengths.data(),
                                h->last_is_log, st);
         if (rc) return rc;
-        return asr_ctc_get_beams(h->wide, max_hyps, max_len, n_hyps, lengths, labels, logp);
+        return asr_ctc_get_beams_ts(h->wide, max_hyps, max_len, n_hyps, lengths, labels, logp, timesteps);
     }
     std::vector<std::vector<int>> fwd;
     for (int b = 0; b < B; b++) {
@@ -703,6 +743,10 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyps, 
             if (labels)
                 for (int x = 0; x < (int)fwd[i].size() && x < max_len; x++)
                     labels[base * max_len + x] = fwd[i][x];
+            if (timesteps) {
+                const int* src = tsv.data() + ((size_t)b * kc + i) * T;
+                for (int x = 0; x < (int)fwd[i].size() && x < max_len; x++) timesteps[base * max_len + x] = src[x];
+            }
         }
     }
     return stc;

@@ -183,6 +183,18 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* h_labels, int max_len, int32_t* h_le
 int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps,
                       int32_t* h_lengths, int32_t* h_labels, double* h_logp);
 
+/* Timesteps mode (ctcdecode's `timesteps` output, baseline/main.py:46; the
+ * reference C++ decoder has none): when on, decodes also record the frame at
+ * which every label of every live prefix was appended (a continuing prefix
+ * keeps its frames; a new prefix is its parent's plus the current frame), at
+ * 16 extra bytes per node record and slot.  Off by default; the one-wave
+ * list kernel is not used while it is on.  asr_ctc_get_beams_ts returns them
+ * as h_timesteps[B][max_hyps][max_len] next to the ranked labels
+ * (ASR_ERR_STATE if the decode ran without timesteps). */
+int asr_ctc_set_timesteps(asr_ctc_t* h, int on);
+int asr_ctc_get_beams_ts(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps,
+                         int32_t* h_lengths, int32_t* h_labels, double* h_logp, int32_t* h_timesteps);
+
 /* Device time of the last decode's beam-search kernel (ms, HIP events on the
  * decode stream) and its launch geometry; for roofline accounting. */
 int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms);

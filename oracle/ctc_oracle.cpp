@@ -83,9 +83,42 @@ struct OracleCTC {
     int vocabSize, beamWidth, blankID;
     std::set<Str> path, updatePath, finalPath;                           // h:48-55
     std::map<Str, S> pathScore, updatePathScore, finalPathScore;
+    // Timesteps (ctcdecode's `timesteps` output, baseline/main.py:46; not in
+    // the reference C++ decoder, so this is the build's own definition,
+    // parity unpinned): the frame at which each label of a prefix was
+    // appended, kept per live PREFIX (state string without its trailing
+    // blank).  A prefix that was live at t-1 keeps its frames; a prefix new
+    // at t is its parent's frames plus t.  Tracked only when track_ts.
+    bool track_ts = false;
+    std::map<Str, std::vector<int>> frames, newFrames;
 
     OracleCTC(const std::vector<char16_t>& c, int beam, int blank)
         : code(c), vocabSize((int)c.size()), beamWidth(beam), blankID(blank) {}
+
+    Str prefix_of(const Str& s) const {
+        Str p = s;
+        if (!p.empty() && p.back() == code[blankID]) p.pop_back();
+        return p;
+    }
+    // frames of the prefix of new state string ns, reached from state s at t
+    void note_frames(const Str& s, const Str& ns, int t) {
+        const Str p = prefix_of(s), np = prefix_of(ns);
+        if (newFrames.count(np)) return;
+        auto f = frames.find(np);
+        if (f != frames.end()) { newFrames[np] = f->second; return; }   // live at t-1 (or np == p)
+        std::vector<int> v = frames[p];
+        v.push_back(t);
+        newFrames[np] = v;
+    }
+    // keep the frames of the prefixes that survived the prune
+    void settle_frames() {
+        frames.clear();
+        for (const Str& s : path) {
+            const Str p = prefix_of(s);
+            frames[p] = newFrames[p];
+        }
+        newFrames.clear();
+    }
 
     // initialPath (cpp:87-95): one state per symbol, then prune.
     void initialPath(const S* le) {
@@ -93,8 +126,10 @@ struct OracleCTC {
             Str s(1, code[i]);
             path.insert(s);
             pathScore.insert(std::make_pair(s, le[i]));
+            if (track_ts) newFrames[prefix_of(s)] = i == blankID ? std::vector<int>() : std::vector<int>(1, 0);
         }
         prune();
+        if (track_ts) settle_frames();
     }
 
     // prune (cpp:97-118) with F1/F2: keep states scoring >= the
@@ -116,7 +151,7 @@ struct OracleCTC {
     }
 
     // extend (cpp:120-167): every state x every symbol, merged by string.
-    void extend(const S* le) {
+    void extend(const S* le, int t = 0) {
         updatePathScore.clear();
         updatePath.clear();
         const char16_t blankCh = code[blankID];
@@ -136,6 +171,7 @@ struct OracleCTC {
                     newPath = s + code[i];
                 }
                 const S score = P::extend(sc, le[i]);
+                if (track_ts) note_frames(s, newPath, t);
                 auto f = updatePathScore.find(newPath);            // cpp:159-164
                 if (f != updatePathScore.end()) {
                     f->second = P::merge(f->second, score);
@@ -169,11 +205,14 @@ struct OracleCTC {
         path.clear(); pathScore.clear();
         finalPath.clear(); finalPathScore.clear();
         initialPath(&le[0]);
+        frames.clear();
+        newFrames.clear();
         for (int t = 1; t < T; t++) {
-            extend(&le[(size_t)t * vocabSize]);
+            extend(&le[(size_t)t * vocabSize], t);
             path = updatePath;                                     // cpp:67-68
             pathScore = updatePathScore;
             prune();                                               // cpp:69
+            if (track_ts) settle_frames();
         }
         mergeIdenticalPaths();                                     // cpp:72
     }
@@ -182,6 +221,7 @@ struct OracleCTC {
 struct Hyp {
     Str s;
     double score;
+    std::vector<int> ts;   // append frame of each label (track_ts)
 };
 
 // Final hypotheses ranked by (score desc, string asc).  Rank 0 is exactly
@@ -190,7 +230,10 @@ struct Hyp {
 template <class P>
 std::vector<Hyp> ranked(const OracleCTC<P>& d) {
     std::vector<Hyp> h;
-    for (const auto& kv : d.finalPathScore) h.push_back({kv.first, (double)kv.second});
+    for (const auto& kv : d.finalPathScore) {
+        auto f = d.frames.find(kv.first);
+        h.push_back({kv.first, (double)kv.second, f != d.frames.end() ? f->second : std::vector<int>()});
+    }
     std::stable_sort(h.begin(), h.end(), [](const Hyp& a, const Hyp& b) {
         return a.score > b.score;   // stable: ties keep map (string) order
     });
@@ -204,7 +247,8 @@ namespace {
 template <class P>
 int decode_all(const float* emis, int T, int B, int V, int beam, int blank,
                const int32_t* codes, int is_log, int nthreads, int max_hyps, int max_len,
-               int32_t* n_hyps, int32_t* lengths, int32_t* labels, double* logp) {
+               int32_t* n_hyps, int32_t* lengths, int32_t* labels, double* logp,
+               int32_t* timesteps = nullptr) {
     if (!emis || T < 1 || B < 1 || V < 2 || beam < 1 || blank < 0 || blank >= V ||
         max_hyps < 1 || max_len < 1)
         return -1;
@@ -219,6 +263,7 @@ int decode_all(const float* emis, int T, int B, int V, int beam, int blank,
     if (nthreads > B) nthreads = B;
     auto work = [&](int b0, int b1) {
         OracleCTC<P> dec(code, beam, blank);
+        dec.track_ts = timesteps != nullptr;
         std::vector<typename P::S> le((size_t)T * V);
         for (int b = b0; b < b1; b++) {
             for (int t = 0; t < T; t++)
@@ -233,8 +278,10 @@ int decode_all(const float* emis, int T, int B, int V, int beam, int blank,
                 size_t base = (size_t)b * max_hyps + k;
                 lengths[base] = (int32_t)h[k].s.size();
                 logp[base] = h[k].score;
-                for (int i = 0; i < (int)h[k].s.size() && i < max_len; i++)
+                for (int i = 0; i < (int)h[k].s.size() && i < max_len; i++) {
                     labels[base * max_len + i] = label_of[h[k].s[i]];
+                    if (timesteps) timesteps[base * max_len + i] = i < (int)h[k].ts.size() ? h[k].ts[i] : -1;
+                }
             }
         }
     };
@@ -267,6 +314,18 @@ int oracle_ctc_decode(const float* emis, int T, int B, int V, int beam, int blan
                       double* logp) {
     return decode_all<LogDomain>(emis, T, B, V, beam, blank, codes, is_log, nthreads,
                                  max_hyps, max_len, n_hyps, lengths, labels, logp);
+}
+
+// The same with the append frame of every label of every hypothesis
+// (timesteps[B][max_hyps][max_len]; the build's definition of ctcdecode's
+// timesteps, see OracleCTC::track_ts).
+int oracle_ctc_decode_ts(const float* emis, int T, int B, int V, int beam, int blank,
+                         const int32_t* codes, int is_log, int nthreads, int max_hyps,
+                         int max_len, int32_t* n_hyps, int32_t* lengths, int32_t* labels,
+                         double* logp, int32_t* timesteps) {
+    if (!timesteps) return -1;
+    return decode_all<LogDomain>(emis, T, B, V, beam, blank, codes, is_log, nthreads,
+                                 max_hyps, max_len, n_hyps, lengths, labels, logp, timesteps);
 }
 
 // The reference's literal arithmetic (fp32 probability products and sums)

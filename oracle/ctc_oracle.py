@@ -39,6 +39,8 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.argtypes = [vp, i, i, i, i, i, vp, i, i, i, i, vp, vp, vp, vp]
             fn.restype = i
+        L.oracle_ctc_decode_ts.argtypes = [vp, i, i, i, i, i, vp, i, i, i, i, vp, vp, vp, vp, vp]
+        L.oracle_ctc_decode_ts.restype = i
         L.oracle_ctc_time.argtypes = [vp, i, i, i, i, i, i, i]
         L.oracle_ctc_time.restype = ctypes.c_double
         _lib = L
@@ -67,6 +69,29 @@ def decode(emis: np.ndarray, beam: int, blank: int = 0, codes: Optional[Sequence
         raise ValueError("oracle_ctc_decode: bad arguments")
     return [[(list(lab[b, k, :ln[b, k]]), float(lp[b, k])) for k in range(min(nh[b], max_hyps))]
             for b in range(B)]
+
+
+def decode_ts(emis: np.ndarray, beam: int, blank: int = 0, codes: Optional[Sequence[int]] = None,
+              is_log: bool = False, nthreads: int = 1, max_hyps: int = 512):
+    """Ranked final beam [(labels, logp, timesteps)] per utterance: timesteps[i]
+    is the frame at which label i was appended (OracleCTC::track_ts; the
+    build's definition of ctcdecode's timesteps, parity unpinned)."""
+    emis = np.ascontiguousarray(emis, dtype=np.float32)
+    T, B, V = emis.shape
+    c = None if codes is None else np.ascontiguousarray(codes, dtype=np.int32)
+    nh = np.zeros(B, np.int32)
+    ln = np.zeros((B, max_hyps), np.int32)
+    lab = np.zeros((B, max_hyps, T), np.int32)
+    lp = np.zeros((B, max_hyps), np.float64)
+    ts = np.full((B, max_hyps, T), -1, np.int32)
+    rc = lib().oracle_ctc_decode_ts(emis.ctypes.data, T, B, V, beam, blank,
+                                    c.ctypes.data if c is not None else None, int(is_log), nthreads,
+                                    max_hyps, T, nh.ctypes.data, ln.ctypes.data, lab.ctypes.data,
+                                    lp.ctypes.data, ts.ctypes.data)
+    if rc != 0:
+        raise ValueError("oracle_ctc_decode_ts: bad arguments")
+    return [[(list(lab[b, k, :ln[b, k]]), float(lp[b, k]), list(ts[b, k, :ln[b, k]]))
+             for k in range(min(nh[b], max_hyps))] for b in range(B)]
 
 
 def time_decode(emis: np.ndarray, beam: int, blank: int = 0, is_log: bool = False,

@@ -74,6 +74,13 @@ def test_ctcdecode_style_mirror_numpy_and_torch_gpu():
             assert out_lens[b, k] == len(lab)
             assert list(res[b, k, :len(lab)]) == lab
             assert abs(float(scores[b, k]) + lp) <= 1e-5 * max(1.0, abs(lp))
+    # timesteps: each label's append frame, as the oracle tracks it
+    for b in range(B):
+        ref_ts = oracle.decode_ts(np.ascontiguousarray(emis[:lens[b], b:b + 1, :]), beam, 0, is_log=True)[0]
+        for k in range(beam):
+            lab, _, ts = ref_ts[k]
+            assert list(steps[b, k, :len(lab)]) == ts, f"utterance {b} hypothesis {k}: timesteps differ"
+            assert all(steps[b, k, len(lab):] == -1)
     # a GPU tensor is decoded in place (no host copy) and gives the same beams
     res2, scores2, _, lens2 = dec.decode(torch.from_numpy(probs_btv).cuda(), torch.from_numpy(lens))
     assert np.array_equal(res, res2) and np.array_equal(scores, scores2) and np.array_equal(out_lens, lens2)

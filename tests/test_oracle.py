@@ -139,3 +139,22 @@ def test_oracle_under_sanitizers():
                        timeout=300, env={**__import__("os").environ, "ASAN_OPTIONS": "detect_leaks=1"})
     assert r.returncode == 0, r.stdout + r.stderr
     assert "oracle sanitizer run: ok" in r.stdout
+
+
+def test_oracle_timesteps_properties():
+    """The oracle's timesteps (ctcdecode's output, the build's definition):
+    one per label, strictly increasing frames < T, the same beams as the
+    plain decode, and a label's frame never later than where a hypothesis
+    sharing that prefix appended it (prefixes share frames)."""
+    T, B, V, beam = 40, 3, 7, 8
+    emis = oracle.synthetic_emissions(T, B, V, seed0=12)
+    ts = oracle.decode_ts(emis, beam, 0, nthreads=2)
+    plain = oracle.decode(emis, beam, 0, nthreads=2)
+    for u_ts, u in zip(ts, plain):
+        assert [(l, s) for l, s, _ in u_ts] == u
+        for lab, _, fr in u_ts:
+            assert len(fr) == len(lab)
+            assert all(0 <= a < b < T for a, b in zip(fr, fr[1:]))
+    # T = 1: every hypothesis is one label appended at frame 0
+    one = oracle.decode_ts(emis[:1], beam, 0)
+    assert all(fr == [0] * len(lab) for u in one for lab, _, fr in u)
