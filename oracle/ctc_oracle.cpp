@@ -204,9 +204,9 @@ struct OracleCTC {
     void decode(const std::vector<S>& le, int T) {
         path.clear(); pathScore.clear();
         finalPath.clear(); finalPathScore.clear();
-        initialPath(&le[0]);
         frames.clear();
         newFrames.clear();
+        initialPath(&le[0]);
         for (int t = 1; t < T; t++) {
             extend(&le[(size_t)t * vocabSize], t);
             path = updatePath;                                     // cpp:67-68
