@@ -1,0 +1,11 @@
+#!/bin/bash
+set -u
+O=gpurun_out/r2g13
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_ctc_timesteps_gpu.py tests/test_ctc_batch_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_ts.log 2>&1 || { echo "ts tests failed"; grep -E "FAILED|Error|assert" $O/pytest_ts.log | head -20; tail -5 $O/pytest_ts.log; exit 1; }
+tail -1 $O/pytest_ts.log
+timeout -k 10 900 python -u -m pytest tests/test_ctc_gpu.py tests/test_ctc_cu_semantics.py tests/test_ctc_list_gpu.py tests/test_ctc_wide_gpu.py tests/test_dropin.py tests/test_full_configs_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 200 python tools/ctc_profile.py --waves 8 --cases c2,c3,c5 --sigmas bench,3 --reps 3 > $O/timing.log 2>&1 || { echo "timing failed"; tail -5 $O/timing.log; exit 1; }
+grep -hv amdgpu $O/timing.log | cut -c1-160
+echo done
