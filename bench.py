@@ -221,7 +221,7 @@ def cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (weak scaling)")
@@ -238,6 +238,9 @@ def main():
                     help="skip the rank-0 1-GPU re-decode of the gathered shards")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run RNN and decode of each step back to back on one stream")
+    ap.add_argument("--cu-split", default="auto", choices=["auto", "none", "half", "interleave"],
+                    help="production and decode streams on disjoint CU masks (auto: halves when "
+                         "the batch's decode workgroups fit in half of the CUs)")
     ap.add_argument("--overlap-results", action="store_true",
                     help="queue batch i+1's decode before reading batch i's results "
                          "(measured slower on MI355X: see DESIGN.md §9)")
@@ -291,11 +294,20 @@ def main():
     if pipeline:   # HIP streams/events via torch (same HIP runtime as libasr_amd)
         torch.cuda.set_device(local)
         s_prod, s_dec = torch.cuda.Stream(), torch.cuda.Stream()
+        ncu = torch.cuda.get_device_properties(local).multi_processor_count
+        split = args.cu_split
+        if split == "auto":   # one decode workgroup per utterance, one per CU
+            split = "half" if B <= ncu // 2 else "none"
+        if split != "none":   # the RNN's workgroups then never share a CU with the decoder's
+            s_prod, s_dec = cu_masked_streams(split)
+        split_note = {"none": "", "half": "; decode on CUs [0, n/2), production on [n/2, n)",
+                      "interleave": "; decode on even CUs, production on odd"}[split]
         ev_ready = [torch.cuda.Event() for _ in range(nbuf)]
         ev_free = [torch.cuda.Event() for _ in range(nbuf)]
         prod_stream, dec_stream = s_prod.cuda_stream, s_dec.cuda_stream
     else:
         prod_stream = dec_stream = 0
+        split_note = ""
 
     def produce(k, x=d_x, nb=B):
         """RNN forward + emission projection of a batch into buffer k."""
@@ -438,7 +450,7 @@ def main():
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
-                                    "on another" if pipeline else "none (sequential)")},
+                                    "on another" + split_note if pipeline else "none (sequential)")},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "gather": gather,
         }
         print(json.dumps(line), flush=True)
@@ -446,6 +458,32 @@ def main():
         dist.destroy_process_group()
     for d in decs:
         d.close()
+
+
+def cu_masked_streams(mode):
+    """Two HIP streams restricted to disjoint halves of the GPU's CUs
+    (hipExtStreamCreateWithCUMask), wrapped as torch external streams:
+    (production, decode)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    words = (ncu + 31) // 32
+    masks = []
+    for half in (0, 1):
+        m = [0] * words
+        for cu in range(ncu):
+            take = (cu < ncu // 2) if mode == "half" else (cu % 2 == 0)
+            if take == (half == 1):
+                m[cu // 32] |= 1 << (cu % 32)
+        masks.append((ctypes.c_uint32 * words)(*m))
+    out = []
+    for m in masks:
+        st = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), m)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+        out.append(torch.cuda.ExternalStream(st.value))
+    return out[0], out[1]
 
 
 def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V, reps=10):
