@@ -30,6 +30,7 @@ checked bit for bit against a 1-GPU decode of the same utterance ids on rank
                     [--global-batch G] [--decode-only] [--no-pipeline]
 """
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -458,6 +459,8 @@ def main():
         dist.destroy_process_group()
     for d in decs:
         d.close()
+    asr.synchronize()
+    destroy_raw_streams()
 
 
 def cu_masked_streams(mode):
@@ -482,8 +485,21 @@ def cu_masked_streams(mode):
         rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), m)
         if rc != 0:
             raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+        _RAW_STREAMS.append((hip, st.value))
         out.append(torch.cuda.ExternalStream(st.value))
     return out[0], out[1]
+
+
+_RAW_STREAMS = []
+
+
+def destroy_raw_streams():
+    """Destroy the CU-masked streams before the HIP runtime tears down (a
+    stream left to the runtime's exit handlers crashed a profiled run)."""
+    while _RAW_STREAMS:
+        hip, st = _RAW_STREAMS.pop()
+        hip.hipStreamSynchronize(ctypes.c_void_p(st))
+        hip.hipStreamDestroy(ctypes.c_void_p(st))
 
 
 def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V, reps=10):

@@ -8,7 +8,7 @@ set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${PROF_OUT:-r02prof}
 mkdir -p $OUT
-ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace failed $?"; exit 1; }
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 || { echo "fetch pass failed $?"; exit 1; }
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1 || { echo "write pass failed $?"; exit 1; }
