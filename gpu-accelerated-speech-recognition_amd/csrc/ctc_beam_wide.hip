@@ -1,5 +1,6 @@
 // Instantiations of the large-vocabulary beam-search kernel (V+1 > 64
-// columns, ctc_wide_kernel.inc): 8 waves, 1/2/4 rows per thread.
+// columns, ctc_wide_kernel.inc): 8 waves, 1/2/4 rows per thread, CPU or
+// .cu semantics.
 #include "ctc_wide_kernel.inc"
 
 namespace asr {
@@ -7,9 +8,17 @@ namespace asr {
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s) {
     const size_t lds = ctc_lds_bytes(a.g);
     const dim3 grid(a.B), block(WNT);
-    if (rpt == 1) { hipLaunchKernelGGL((ctc_wide_kernel<1>), grid, block, lds, s, a); ASR_LAUNCH_TRY(); return ASR_OK; }
-    if (rpt == 2) { hipLaunchKernelGGL((ctc_wide_kernel<2>), grid, block, lds, s, a); ASR_LAUNCH_TRY(); return ASR_OK; }
-    if (rpt == 4) { hipLaunchKernelGGL((ctc_wide_kernel<4>), grid, block, lds, s, a); ASR_LAUNCH_TRY(); return ASR_OK; }
+#define ASR_W_LAUNCH(R)                                                                        \
+    if (rpt == R) {                                                                            \
+        if (a.cu_mode) hipLaunchKernelGGL((ctc_wide_kernel<R, true>), grid, block, lds, s, a); \
+        else hipLaunchKernelGGL((ctc_wide_kernel<R, false>), grid, block, lds, s, a);          \
+        ASR_LAUNCH_TRY();                                                                      \
+        return ASR_OK;                                                                         \
+    }
+    ASR_W_LAUNCH(1)
+    ASR_W_LAUNCH(2)
+    ASR_W_LAUNCH(4)
+#undef ASR_W_LAUNCH
     return ASR_ERR_UNSUPPORTED;
 }
 
@@ -23,9 +32,11 @@ size_t ctc_lds_bytes_wide(int kc, int V) {
 
 int ctc_set_max_lds_wide() {
     const int lim = 160 * 1024;
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wide_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wide_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wide_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+#define ASR_W_ATTR(R, C) \
+    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wide_kernel<R, C>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    ASR_W_ATTR(1, false) ASR_W_ATTR(2, false) ASR_W_ATTR(4, false)
+    ASR_W_ATTR(1, true) ASR_W_ATTR(2, true) ASR_W_ATTR(4, true)
+#undef ASR_W_ATTR
     return ASR_OK;
 }
 

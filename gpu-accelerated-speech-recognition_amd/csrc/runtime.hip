@@ -494,7 +494,6 @@ int asr_ctc_destroy(asr_ctc_t* h) {
 int asr_ctc_set_semantics(asr_ctc_t* h, int semantics) {
     if (!h || (semantics != ASR_CTC_SEMANTICS_CPU && semantics != ASR_CTC_SEMANTICS_CUDA))
         return ASR_ERR_ARG;
-    if (semantics == ASR_CTC_SEMANTICS_CUDA && h->V + 1 > 64) return ASR_ERR_UNSUPPORTED;
     h->cu_mode = semantics == ASR_CTC_SEMANTICS_CUDA ? 1 : 0;
     h->K = h->cu_mode ? h->beam : h->beam + 1;   // exactly beam states vs beam+1 and ties
     h->have = false;

@@ -205,7 +205,8 @@ int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms);
  * exactly min(beam, n) states per step (stable descending sort, cu:174-196;
  * ties at the cutoff resolved in a fixed slot order instead of the .cu's
  * string order), and on the last step the trailing blank is stripped before
- * the merge and the prune (cu:452-456).  V <= 63 only. */
+ * the merge and the prune (cu:452-456).  Any V (the reference's char vocabs
+ * have up to 256 symbols, CTCBeamSearch.h:43). */
 enum { ASR_CTC_SEMANTICS_CPU = 0, ASR_CTC_SEMANTICS_CUDA = 1 };
 int asr_ctc_set_semantics(asr_ctc_t* h, int semantics);
 
