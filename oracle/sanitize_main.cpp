@@ -24,6 +24,8 @@ int oracle_ctc_decode(const float*, int, int, int, int, int, const int32_t*, int
 int oracle_ctc_decode_prob(const float*, int, int, int, int, int, const int32_t*, int, int, int,
                            int, int32_t*, int32_t*, int32_t*, double*);
 double oracle_ctc_time(const float*, int, int, int, int, int, int, int);
+int oracle_ctc_decode_ts(const float*, int, int, int, int, int, const int32_t*, int, int, int, int,
+                         int32_t*, int32_t*, int32_t*, double*, int32_t*);
 }
 
 namespace {
@@ -111,6 +113,24 @@ int main() {
     }
     // large vocabulary, wide beam (C5-like, short T)
     run(emissions(5, 2, 300, 8, 3.0, false), 5, 2, 300, 40, 0, nullptr, 0, 2, 64, 5, false);
+    // timesteps (ctcdecode's output): one strictly increasing frame < T per label
+    {
+        const int T = 25, B = 3, V = 11, beam = 6, mh = 16;
+        std::vector<float> e = emissions(T, B, V, 10, 3.0, false);
+        std::vector<int32_t> nh(B), len((size_t)B * mh), lab((size_t)B * mh * T), ts((size_t)B * mh * T);
+        std::vector<double> lp((size_t)B * mh);
+        expect(oracle_ctc_decode_ts(e.data(), T, B, V, beam, 0, nullptr, 0, 2, mh, T, nh.data(), len.data(),
+                                    lab.data(), lp.data(), ts.data()) == 0, "ts rc", T, V, beam);
+        for (int b = 0; b < B; b++)
+            for (int k = 0; k < std::min(nh[b], mh); k++) {
+                const size_t base = (size_t)b * mh + k;
+                for (int i = 0; i < len[base]; i++) {
+                    const int f = ts[base * T + i];
+                    expect(f >= 0 && f < T && (i == 0 || f > ts[base * T + i - 1]), "timesteps increasing",
+                           T, V, beam);
+                }
+            }
+    }
     // timing entry point
     {
         std::vector<float> e = emissions(8, 2, 29, 9, 3.0, false);
