@@ -44,6 +44,7 @@ struct CtcArgs {
     int* best_len;          // [B]
     double* best_score;     // [B]
     uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
+    uint32_t* tile0;        // [B][T][WREC] first label tile per frame (wide kernel, V > 65; NULL: in-kernel)
 };
 
 int ctc_row_capacity(int kcap);   // compile-time slot capacity KC >= kcap (64, 128, 256)
@@ -56,6 +57,7 @@ int ctc_set_max_lds_v32();
 int ctc_set_max_lds_v64();
 constexpr int WIDE_VMAX = 4096;   // largest vocabulary of the wide kernel (ctc_wide_kernel.inc)
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
+size_t ctc_tile0_bytes(int B, int T);   // a.tile0 workspace of the wide kernel
 size_t ctc_lds_bytes_wide(int kc, int V);
 int ctc_set_max_lds_wide();
 // One wave per utterance, list-based (ctc_wave_kernel.inc): the default when supported.

@@ -5,7 +5,15 @@
 
 namespace asr {
 
+size_t ctc_tile0_bytes(int B, int T) { return sizeof(uint32_t) * WREC * (size_t)B * T; }
+
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s) {
+    if (a.tile0) {   // every frame's first tile (ctc_tile0_kernel), then the decode
+        if (a.g.V - 1 <= WTILE || a.g.V > WVMAX) return ASR_ERR_ARG;
+        hipLaunchKernelGGL(ctc_tile0_kernel, dim3((unsigned)(a.B * a.T)), dim3(64), sizeof(uint32_t) * a.g.V, s, a,
+                           a.tile0);
+        ASR_LAUNCH_TRY();
+    }
     const size_t lds = ctc_lds_bytes(a.g);
     const dim3 grid(a.B), block(WNT);
 #define ASR_W_LAUNCH(R)                                                                        \

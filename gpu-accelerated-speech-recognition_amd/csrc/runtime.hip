@@ -299,6 +299,8 @@ struct asr_ctc {
     int ts = 0;                      // timesteps mode (asr_ctc_set_timesteps)
     int4* d_nodes_ts = nullptr;      // [B][T*kcap] append frames per node record
     uint64_t* d_fin_ts = nullptr;    // [B][kcap][2] append frames of the final tails
+    uint32_t* d_tile0 = nullptr;     // [B][T] first label tile per frame (wide kernel, V > 65)
+    bool tile0 = true;               // precompute first tiles (ASR_CTC_TILE0=0: in-kernel, for A/B timing)
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
     unsigned char* h_res = nullptr;   // pinned mirror of d_res
@@ -363,8 +365,8 @@ void free_ws(asr_ctc* h) {
     hipFree(h->d_fin_tail); hipFree(h->d_chain);
     h->d_fin_tail = nullptr; h->d_chain = nullptr;
     hipFree(h->d_fin_score); hipFree(h->d_res);
-    hipFree(h->d_nodes_ts); hipFree(h->d_fin_ts);
-    h->d_nodes_ts = nullptr; h->d_fin_ts = nullptr;
+    hipFree(h->d_nodes_ts); hipFree(h->d_fin_ts); hipFree(h->d_tile0);
+    h->d_nodes_ts = nullptr; h->d_fin_ts = nullptr; h->d_tile0 = nullptr;
     hipHostFree(h->h_res);
     h->d_res = nullptr; h->h_res = nullptr;
     h->d_nodes = nullptr; h->d_fin_n = h->d_fin_node = h->d_status = nullptr;
@@ -372,6 +374,10 @@ void free_ws(asr_ctc* h) {
     h->h_best_lab = h->h_best_len = h->h_status = nullptr; h->h_best_score = nullptr;
     h->capB = h->capT = 0;
 }
+
+// The wide kernel (V + 1 > 64) takes every frame's first tile from a
+// precompute pass when the vocabulary spans more than one tile.
+bool use_tile0(const asr_ctc* h) { return h->tile0 && h->V - 1 > 64 && h->V <= asr::WIDE_VMAX; }
 
 int ensure_ws(asr_ctc* h, int B, int T) {
     if (B <= h->capB && T <= h->capT) {
@@ -400,6 +406,7 @@ int ensure_ws(asr_ctc* h, int B, int T) {
         ASR_HIP_TRY(hipMalloc(&h->d_nodes_ts, sizeof(int4) * (size_t)nB * nT * kc));
         ASR_HIP_TRY(hipMalloc(&h->d_fin_ts, sizeof(uint64_t) * 2 * (size_t)nB * kc));
     }
+    if (use_tile0(h)) ASR_HIP_TRY(hipMalloc(&h->d_tile0, asr::ctc_tile0_bytes(nB, nT)));
     h->capB = nB;
     h->capT = nT;
     return ASR_OK;
@@ -457,6 +464,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     h->kcap = kcap;
     h->waves_override = 0;
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
+    if (const char* t0 = getenv("ASR_CTC_TILE0")) h->tile0 = atoi(t0) != 0;
     if (asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }
@@ -577,6 +585,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.fin_score = h->d_fin_score;
     a.nodes_ts = h->ts ? h->d_nodes_ts : nullptr;
     a.fin_ts = h->ts ? h->d_fin_ts : nullptr;
+    a.tile0 = use_tile0(h) ? h->d_tile0 : nullptr;
     // packed result layout for this (B, T)
     h->d_best_score = reinterpret_cast<double*>(h->d_res);
     h->d_best_len = reinterpret_cast<int*>(h->d_res + 8 * (size_t)B);

@@ -111,3 +111,35 @@ def test_wide_c5_longer():
     emis = oracle.synthetic_emissions(T, B, V, seed0=16)
     ref = oracle.decode(emis, beam, 0, nthreads=cpu_threads(), max_hyps=beam + 1)
     assert_beams_equal([x[:beam + 1] for x in gpu_beams(emis, beam)], ref, "C5 T=40")
+
+
+@pytest.mark.parametrize("semantics", [asr.SEMANTICS_CPU, asr.SEMANTICS_CUDA])
+def test_wide_tile0_precompute_matches_in_kernel(monkeypatch, semantics):
+    """V > 65: the first tile's threshold of every frame comes from
+    ctc_tile0_kernel (a one-wave radix selection per frame before the
+    decode); ASR_CTC_TILE0=0 makes the decode kernel select it itself.
+    Both give the same beams, bit for bit: on frames whose 12 best labels
+    are continuous and the rest take 6 log levels (ties at every tile
+    threshold, few at the beam cutoff), and on continuous emissions."""
+    T, B, V, beam = 30, 3, 500, 40
+    rng = np.random.default_rng(5)
+    logit = 0.5 * rng.integers(0, 6, size=(T, B, V)).astype(np.float64)
+    for t in range(T):
+        for b in range(B):
+            logit[t, b, rng.permutation(V)[:12]] = 4.0 + 3.0 * rng.random(12)
+    q = np.exp(logit)
+    cases = {"tied tail": (q / q.sum(-1, keepdims=True)).astype(np.float32),
+             "continuous": oracle.synthetic_emissions(T, B, V, seed0=77)}
+    for name, emis in cases.items():
+        got = {}
+        for flag in ("1", "0"):
+            monkeypatch.setenv("ASR_CTC_TILE0", flag)
+            dec = asr.CTCDecoder(V, beam, 0)
+            dec.set_semantics(semantics)
+            dec.decode(emis)
+            got[flag] = dec.beams(max_hyps=dec.config()[0])
+            dec.close()
+        assert got["1"] == got["0"], name
+        if semantics == asr.SEMANTICS_CPU:
+            ref = oracle.decode(emis, beam, 0, nthreads=cpu_threads())
+            assert_beams_equal(got["1"], ref, name)

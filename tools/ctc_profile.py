@@ -22,6 +22,9 @@ oracle = _load("ctc_oracle", ROOT / "oracle" / "ctc_oracle.py")
 PHASES = ["chunk", "P1 cand", "P2a folds>=G", "P2b select", "P2c fallback", "P3a scan",
           "P3b+barrier", "n:orphan inserts", "n:orphan filter hits", "n:extensions", "radix:pre-barrier",
           "radix:barrier", "radix:post", "-", "-", "-"]
+WIDE_PHASES = ["staging+pool", "tile threshold", "tile labels+child", "stage1", "exact+stage2",
+               "pool write", "slots", "n:tiles", "candidates", "n:keys in stage-1 window", "radix:pre-barrier", "radix:barrier",
+               "radix:post", "-", "-", "-"]   # ctc_wide_kernel.inc (V > 63)
 COUNTERS = True   # slots 13-15 of the stamps build are counters
 
 
@@ -92,14 +95,15 @@ def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         asr.check(fn(dec.h, buf.ctypes.data), "stamps")
         per = buf.astype(np.float64).mean(axis=0) / T
-        out["cycles_per_step"] = {PHASES[i]: round(per[i], 1) for i in range(13)
-                                  if PHASES[i] != "-" and not PHASES[i].startswith("n:")}
-        out["events_per_frame"] = {PHASES[i][2:]: round(per[i], 2) for i in range(13) if PHASES[i].startswith("n:")}
+        PH = WIDE_PHASES if V + 1 > 64 else PHASES
+        out["cycles_per_step"] = {PH[i]: round(per[i], 1) for i in range(13)
+                                  if PH[i] != "-" and not PH[i].startswith("n:")}
+        out["events_per_frame"] = {PH[i][2:]: round(per[i], 2) for i in range(13) if PH[i].startswith("n:")}
         ranks = (buf[:, 15] & 0xFFFFFFFF).astype(np.float64)
         out["per_frame"] = {"fallbacks": round(per[13], 4), "exact_passes": round(per[14], 3),
                             "ranks": round(ranks.mean() / T, 3),
                             "mean_cd": round(float((buf[:, 15] >> 32).sum() / max(1.0, ranks.sum())), 2)}
-        out["cycles_total"] = round(per[:7].sum(), 1)
+        out["cycles_total"] = round(per[:7].sum() + (per[8] if PH is WIDE_PHASES else 0.0), 1)
     dec.close()
     return out
 
