@@ -19,6 +19,8 @@ pytestmark = pytest.mark.gpu
     (25, 3, 300, 50),       # C5-like width, C2 beam
     (40, 2, 129, 5),
     (10, 2, 1000, 200),     # BASELINE C5 vocabulary and beam
+    (8, 2, 4096, 50),       # largest vocabulary
+    (6, 2, 4096, 200),      # ... and beam: little LDS left for window segments (fallback path)
 ])
 def test_wide_random_parity(T, B, V, beam):
     emis = oracle.synthetic_emissions(T, B, V, seed0=3000 + T + V + beam)
