@@ -239,9 +239,11 @@ def main():
                     help="skip the rank-0 1-GPU re-decode of the gathered shards")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run RNN and decode of each step back to back on one stream")
-    ap.add_argument("--cu-split", default="auto", choices=["auto", "none", "half", "interleave"],
-                    help="production and decode streams on disjoint CU masks (auto: halves when "
-                         "the batch's decode workgroups fit in half of the CUs)")
+    ap.add_argument("--cu-split", default="auto", choices=["auto", "none", "half", "fit", "interleave"],
+                    help="production and decode streams on disjoint CU masks (auto: halves when the "
+                         "batch's decode workgroups fit in half of the CUs; fit: one CU per workgroup)")
+    ap.add_argument("--result-stream", action="store_true",
+                    help="run each batch's traceback on a third stream (measured slower at C2)")
     ap.add_argument("--overlap-results", action="store_true",
                     help="queue batch i+1's decode before reading batch i's results "
                          "(measured slower on MI355X: see DESIGN.md §9)")
@@ -298,11 +300,17 @@ def main():
         ncu = torch.cuda.get_device_properties(local).multi_processor_count
         split = args.cu_split
         if split == "auto":   # one decode workgroup per utterance, one per CU
-            split = "half" if B <= ncu // 2 else "none"
+            split = "half" if B <= ncu // 2 else "none"   # fit: equal at C2, slower at C5 (r2g28)
         if split != "none":   # the RNN's workgroups then never share a CU with the decoder's
-            s_prod, s_dec = cu_masked_streams(split)
+            s_prod, s_dec = cu_masked_streams(split, B)
         split_note = {"none": "", "half": "; decode on CUs [0, n/2), production on [n/2, n)",
+                      "fit": f"; decode on CUs [0, {min(ncu, -(-B // 8) * 8)}) (one per utterance), "
+                             "production on the rest",
                       "interleave": "; decode on even CUs, production on odd"}[split]
+        if args.result_stream:   # tracebacks off the decode stream
+            s_res = torch.cuda.Stream()
+            for d in decs:
+                d.set_result_stream(s_res.cuda_stream)
         ev_ready = [torch.cuda.Event() for _ in range(nbuf)]
         ev_free = [torch.cuda.Event() for _ in range(nbuf)]
         prod_stream, dec_stream = s_prod.cuda_stream, s_dec.cuda_stream
@@ -348,14 +356,17 @@ def main():
         prev = None
         for i in range(n):
             k = i % nbuf
+            # batch i's decode is queued first: the host time spent queueing
+            # the production (C5: one recurrence launch per frame) then
+            # overlaps the decode instead of delaying it
+            s_dec.wait_event(ev_ready[k])
+            enqueue(k)
+            ev_free[k].record(s_dec)
             if i + 1 < n:   # batch i+1 is produced while batch i is decoded
                 kn = (i + 1) % nbuf
                 s_prod.wait_event(ev_free[kn])
                 produce(kn)
                 ev_ready[kn].record(s_prod)
-            s_dec.wait_event(ev_ready[k])
-            enqueue(k)
-            ev_free[k].record(s_dec)
             if not args.overlap_results:
                 collect(k)
                 continue
@@ -451,7 +462,9 @@ def main():
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
-                                    "on another" + split_note if pipeline else "none (sequential)")},
+                                    "on another" + split_note +
+                                    ("; tracebacks on a third stream" if args.result_stream else "")
+                                    if pipeline else "none (sequential)")},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "gather": gather,
         }
         print(json.dumps(line), flush=True)
@@ -463,10 +476,11 @@ def main():
     destroy_raw_streams()
 
 
-def cu_masked_streams(mode):
-    """Two HIP streams restricted to disjoint halves of the GPU's CUs
+def cu_masked_streams(mode, B=0):
+    """Two HIP streams restricted to disjoint sets of the GPU's CUs
     (hipExtStreamCreateWithCUMask), wrapped as torch external streams:
-    (production, decode)."""
+    (production, decode).  half: [0, n/2) decodes; fit: [0, B rounded up
+    to 8) decodes (one workgroup per utterance); interleave: even CUs."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
@@ -475,7 +489,12 @@ def cu_masked_streams(mode):
     for half in (0, 1):
         m = [0] * words
         for cu in range(ncu):
-            take = (cu < ncu // 2) if mode == "half" else (cu % 2 == 0)
+            if mode == "half":
+                take = cu < ncu // 2
+            elif mode == "fit":
+                take = cu < min(ncu, -(-B // 8) * 8)
+            else:
+                take = cu % 2 == 0
             if take == (half == 1):
                 m[cu // 32] |= 1 << (cu % 32)
         masks.append((ctypes.c_uint32 * words)(*m))

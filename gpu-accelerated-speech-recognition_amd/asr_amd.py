@@ -52,7 +52,7 @@ EXPORTS = [
     "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
-    "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts",
+    "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
 ]
 
 
@@ -116,6 +116,7 @@ def lib() -> ctypes.CDLL:
         "asr_ctc_decode_ex": [_vp, _vp, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
         "asr_ctc_set_semantics": [_vp, _i],
         "asr_ctc_set_timesteps": [_vp, _i],
+        "asr_ctc_set_result_stream": [_vp, _vp],
         "asr_ctc_get_beams_ts": [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp],
     }
     for name, args in sig.items():
@@ -338,6 +339,11 @@ class CTCDecoder:
         """SEMANTICS_CPU (default, the parity target) or SEMANTICS_CUDA
         (CTCBeamSearch.cu: exactly beam states, strip-then-merge last step)."""
         check(lib().asr_ctc_set_semantics(self.h, semantics), "asr_ctc_set_semantics")
+
+    def set_result_stream(self, stream: int) -> None:
+        """Run the best-path traceback and its copy to host memory on `stream`
+        (a hipStream_t handle; 0: the decode's own stream)."""
+        check(lib().asr_ctc_set_result_stream(self.h, ctypes.c_void_p(stream or None)), "asr_ctc_set_result_stream")
 
     def set_timesteps(self, on: bool) -> None:
         """Record each label's append frame in later decodes (beams_ts)."""

@@ -312,6 +312,9 @@ struct asr_ctc {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_res = nullptr;    // traceback done, results in the pinned mirror
+    hipEvent_t ev_dec = nullptr;    // decode done (fork to the result stream)
+    hipStream_t res_stream = nullptr;   // traceback + result copy (asr_ctc_set_result_stream); null: the decode's
+    bool res_fork = false;          // a traceback was queued on res_stream
     asr::CtcArgs args{};
     uint64_t* d_stamps = nullptr;   // diagnostic build only
     int cap_stamps = 0;
@@ -472,7 +475,8 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
         hipMalloc(&h->d_codes, sizeof(int) * V) != hipSuccess ||
         hipMemcpy(h->d_codes, h->codes.data(), sizeof(int) * V, hipMemcpyHostToDevice) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_res, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->ev_res, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_dec, hipEventDisableTiming) != hipSuccess) {
         delete h;
         return ASR_ERR_HIP;
     }
@@ -495,6 +499,7 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
     if (h->ev_res) hipEventDestroy(h->ev_res);
+    if (h->ev_dec) hipEventDestroy(h->ev_dec);
     delete h;
     return ASR_OK;
 }
@@ -505,6 +510,12 @@ int asr_ctc_set_semantics(asr_ctc_t* h, int semantics) {
     h->cu_mode = semantics == ASR_CTC_SEMANTICS_CUDA ? 1 : 0;
     h->K = h->cu_mode ? h->beam : h->beam + 1;   // exactly beam states vs beam+1 and ties
     h->have = false;
+    return ASR_OK;
+}
+
+int asr_ctc_set_result_stream(asr_ctc_t* h, asr_stream_t s) {
+    if (!h) return ASR_ERR_ARG;
+    h->res_stream = s ? asr_stream(s) : nullptr;
     return ASR_OK;
 }
 
@@ -608,18 +619,29 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.stamps = h->d_stamps;
 #endif
     const hipStream_t st = asr_stream(s);
+    // the previous traceback of this handle (on the result stream) reads the
+    // node records this decode overwrites
+    if (h->res_fork) ASR_HIP_TRY(hipStreamWaitEvent(st, h->ev_res, 0));
     ASR_HIP_TRY(hipEventRecord(h->ev0, st));
     rc = asr::ctc_launch_decode(a, waves, st);
     if (rc) return rc;
     ASR_HIP_TRY(hipEventRecord(h->ev1, st));
-    rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, st);
+    // traceback and result copy: on the result stream when one is set, so
+    // that the decode stream can start the next batch at once
+    const hipStream_t rs = h->res_stream ? h->res_stream : st;
+    h->res_fork = rs != st;
+    if (h->res_fork) {
+        ASR_HIP_TRY(hipEventRecord(h->ev_dec, st));
+        ASR_HIP_TRY(hipStreamWaitEvent(rs, h->ev_dec, 0));
+    }
+    rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, rs);
     if (rc) return rc;
     // One copy of the packed results to the pinned mirror right behind the
     // traceback: asr_ctc_get_best waits for this event only, not for work the
     // caller queued on the stream afterwards (e.g. the next batch's decode).
     ASR_HIP_TRY(hipMemcpyAsync(h->h_res, h->d_res, 16 * (size_t)B + sizeof(int) * (size_t)B * T,
-                               hipMemcpyDeviceToHost, st));
-    ASR_HIP_TRY(hipEventRecord(h->ev_res, st));
+                               hipMemcpyDeviceToHost, rs));
+    ASR_HIP_TRY(hipEventRecord(h->ev_res, rs));
     h->have = true;
     h->last_emis = d_emis;
     h->last_tstride = frame_stride;

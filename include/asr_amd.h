@@ -192,6 +192,14 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps
  * as h_timesteps[B][max_hyps][max_len] next to the ranked labels
  * (ASR_ERR_STATE if the decode ran without timesteps). */
 int asr_ctc_set_timesteps(asr_ctc_t* h, int on);
+
+/* Stream for the best-path traceback and the copy of its results to host
+ * memory (default NULL: the decode's own stream).  With a separate stream
+ * the decode stream is free for the next batch as soon as the beam search
+ * ends; asr_ctc_get_best waits for the results either way, and the next
+ * decode on this handle waits for its traceback.  No reference
+ * counterpart (a scheduling option). */
+int asr_ctc_set_result_stream(asr_ctc_t* h, asr_stream_t s);
 int asr_ctc_get_beams_ts(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps,
                          int32_t* h_lengths, int32_t* h_labels, double* h_logp, int32_t* h_timesteps);
 
