@@ -242,6 +242,10 @@ def main():
     ap.add_argument("--cu-split", default="auto", choices=["auto", "none", "half", "fit", "interleave"],
                     help="production and decode streams on disjoint CU masks (auto: halves when the "
                          "batch's decode workgroups fit in half of the CUs; fit: one CU per workgroup)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches decoded concurrently, each on its own HIP stream and CU group "
+                         "(0 = auto: as many one-CU-per-utterance groups as fit beside production, "
+                         "at most 3; 1 = one decode at a time)")
     ap.add_argument("--result-stream", action="store_true",
                     help="run each batch's traceback on a third stream (measured slower at C2)")
     ap.add_argument("--overlap-results", action="store_true",
@@ -287,35 +291,54 @@ def main():
     d_wout, d_bout = DM(w_out), DM(b_out.reshape(V, 1))
     d_x = DM(make_features(T, B, In, first))
     pipeline = not args.no_pipeline and not args.decode_only
-    # --overlap-results reads batch i-1's results after batch i's decode is
-    # queued, so a third buffer keeps batch i+1's production out of the
-    # emissions batch i-1 may still be re-decoded from (asr_amd.h lifetime rule)
-    nbuf = (3 if args.overlap_results else 2) if pipeline else 1
+    ncu = torch.cuda.get_device_properties(local).multi_processor_count if torch is not None else 256
+    gcu = min(ncu, -(-B // 8) * 8)   # one decode workgroup per utterance, one per CU
+    D = 1
+    if pipeline:
+        # auto: up to 3 decode groups for H <= 256 (C2: 38.7 M vs 21.1 M frames/s at
+        # D = 1), 2 for the H = 1024 recurrence (C5: D = 2 3.48 M, D = 3 2.99 M,
+        # gpurun_out/r2g31); one HIP stream per group plus production stays
+        # within the box's 4 hardware queues (D = 4 at C5: 1.03 M, serialised)
+        D = args.inflight or max(1, min(3 if H <= 256 else 2, ncu // gcu - 1))
+        if D > 1 and (D + 1) * gcu > ncu:
+            raise SystemExit(f"--inflight {D}: {D} decode groups of {gcu} CUs + production exceed {ncu} CUs")
+    # Buffer i % nbuf holds batch i.  D batches are decoding while batch i+1 is
+    # produced, and a buffer is only produced into after its batch's results
+    # were read (asr_amd.h lifetime rule: an overflow retry re-reads it), so
+    # D + 1 buffers (--overlap-results, D = 1: a third one).
+    nbuf = (D + 1 if D > 1 else (3 if args.overlap_results else 2)) if pipeline else 1
     d_hid = [asr.DeviceMatrix(T * B, H) for _ in range(nbuf)]
     d_emis = [asr.DeviceMatrix(T * B, V) for _ in range(nbuf)]
     decs = [asr.CTCDecoder(V, beam, 0, waves=args.waves) for _ in range(nbuf)]
     if pipeline:   # HIP streams/events via torch (same HIP runtime as libasr_amd)
         torch.cuda.set_device(local)
         s_prod, s_dec = torch.cuda.Stream(), torch.cuda.Stream()
-        ncu = torch.cuda.get_device_properties(local).multi_processor_count
+        s_decs = [s_dec]
         split = args.cu_split
-        if split == "auto":   # one decode workgroup per utterance, one per CU
+        if D > 1:
+            split = "groups"
+            s_prod, s_decs = cu_group_streams(D, gcu, ncu)
+            s_dec = s_decs[0]
+        elif split == "auto":   # one decode workgroup per utterance, one per CU
             split = "half" if B <= ncu // 2 else "none"   # fit: equal at C2, slower at C5 (r2g28)
-        if split != "none":   # the RNN's workgroups then never share a CU with the decoder's
+        if split not in ("none", "groups"):   # the RNN's workgroups then never share a CU with the decoder's
             s_prod, s_dec = cu_masked_streams(split, B)
+            s_decs = [s_dec]
         split_note = {"none": "", "half": "; decode on CUs [0, n/2), production on [n/2, n)",
-                      "fit": f"; decode on CUs [0, {min(ncu, -(-B // 8) * 8)}) (one per utterance), "
-                             "production on the rest",
-                      "interleave": "; decode on even CUs, production on odd"}[split]
+                      "fit": f"; decode on CUs [0, {gcu}) (one per utterance), production on the rest",
+                      "interleave": "; decode on even CUs, production on odd",
+                      "groups": f"; {D} batches decoding at once, batch i on stream i % {D} restricted to "
+                                f"CUs [{gcu}*(i % {D}), {gcu}*(i % {D} + 1)) (one per utterance), "
+                                f"production on CUs [{D * gcu}, {ncu})"}[split]
         if args.result_stream:   # tracebacks off the decode stream
             s_res = torch.cuda.Stream()
             for d in decs:
                 d.set_result_stream(s_res.cuda_stream)
         ev_ready = [torch.cuda.Event() for _ in range(nbuf)]
         ev_free = [torch.cuda.Event() for _ in range(nbuf)]
-        prod_stream, dec_stream = s_prod.cuda_stream, s_dec.cuda_stream
+        prod_stream = s_prod.cuda_stream
     else:
-        prod_stream = dec_stream = 0
+        prod_stream = 0
         split_note = ""
 
     def produce(k, x=d_x, nb=B):
@@ -330,9 +353,9 @@ def main():
     kernel_ms = []
     last = {}
 
-    def enqueue(k):
+    def enqueue(k, stream=0):
         """Decode buffer k and its traceback; the results follow to pinned host memory."""
-        decs[k].decode_device(d_emis[k].ptr, T, B, is_log=True, stream=dec_stream)
+        decs[k].decode_device(d_emis[k].ptr, T, B, is_log=True, stream=stream)
 
     def collect(k):
         """Wait for buffer k's results (an event, not the stream) and read them."""
@@ -353,29 +376,39 @@ def main():
         with torch.cuda.stream(s_prod):
             produce(0)
             ev_ready[0].record(s_prod)
-        prev = None
+        lag = D - 1 if D > 1 else (1 if args.overlap_results else 0)
+        pending = []   # buffers decoded, results not read yet (oldest first)
         for i in range(n):
             k = i % nbuf
+            sd = s_decs[i % D]
             # batch i's decode is queued first: the host time spent queueing
             # the production (C5: one recurrence launch per frame) then
             # overlaps the decode instead of delaying it
-            s_dec.wait_event(ev_ready[k])
-            enqueue(k)
-            ev_free[k].record(s_dec)
+            sd.wait_event(ev_ready[k])
+            enqueue(k, sd.cuda_stream)
+            ev_free[k].record(sd)
+            pending.append(k)
             if i + 1 < n:   # batch i+1 is produced while batch i is decoded
                 kn = (i + 1) % nbuf
                 s_prod.wait_event(ev_free[kn])
                 produce(kn)
                 ev_ready[kn].record(s_prod)
-            if not args.overlap_results:
-                collect(k)
-                continue
-            if prev is not None:   # batch i-1's results, while batch i decodes
-                collect(prev)
-            prev = k
-        if prev is not None:
-            collect(prev)
+            # read the oldest batch once `lag` newer ones are decoding behind it
+            while len(pending) > lag:
+                collect(pending.pop(0))
+        while pending:
+            collect(pending.pop(0))
 
+    if pipeline:
+        # every buffer's decoder handle sizes its workspace (hipMalloc, which
+        # synchronises the device) before the warmup: with D batches in flight
+        # the warmup alone may not reach every buffer
+        for k in range(nbuf):
+            produce(k)
+            asr.synchronize()
+            enqueue(k, s_decs[k % D].cuda_stream)
+            collect(k)
+        kernel_ms.clear()
     run(args.warmup)
     kernel_ms.clear()
     if world > 1:
@@ -461,6 +494,7 @@ def main():
                        f": B={B}/GPU (global {GB}), T={T}, hidden={H}, vocab={V}, beam={beam}",
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
+                       "inflight_decodes": D,
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
                                     "on another" + split_note +
                                     ("; tracebacks on a third stream" if args.result_stream else "")
@@ -507,6 +541,28 @@ def cu_masked_streams(mode, B=0):
         _RAW_STREAMS.append((hip, st.value))
         out.append(torch.cuda.ExternalStream(st.value))
     return out[0], out[1]
+
+
+def cu_group_streams(D, gcu, ncu):
+    """D decode streams restricted to the disjoint CU ranges [j*gcu, (j+1)*gcu)
+    and one production stream on [D*gcu, ncu) (hipExtStreamCreateWithCUMask),
+    wrapped as torch external streams: (production, [decode...])."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    words = (ncu + 31) // 32
+    ranges = [(j * gcu, (j + 1) * gcu) for j in range(D)] + [(D * gcu, ncu)]
+    out = []
+    for lo, hi in ranges:
+        m = [0] * words
+        for cu in range(lo, hi):
+            m[cu // 32] |= 1 << (cu % 32)
+        st = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words),
+                                              (ctypes.c_uint32 * words)(*m))
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+        _RAW_STREAMS.append((hip, st.value))
+        out.append(torch.cuda.ExternalStream(st.value))
+    return out[-1], out[:-1]
 
 
 _RAW_STREAMS = []
