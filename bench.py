@@ -8,10 +8,17 @@ already resident in HBM:
     -> best label sequences and log-probs copied to the host.
 Steps are pipelined by default (--no-pipeline: strictly sequential): the RNN
 and emission projection of batch i+1 run on one HIP stream while batch i is
-decoded on another (double-buffered emissions, event-ordered), so the
-recurrence workgroups and the decoder workgroups share the 256 CUs; the
+decoded on another (event-ordered emission buffers), and up to D batches
+decode at once (--inflight D; auto: D = 3 when the batch needs at most a
+quarter of the CUs at one decode workgroup per utterance and H <= 256, as at
+C2; D = 2 at C5), batch i on decode stream i % D, each stream restricted to
+its own group of CUs and the production stream to the rest
+(hipExtStreamCreateWithCUMask).  One utterance is still decoded by one
+workgroup frame after frame; D only lets the decoder workgroups of several
+batches use CUs one batch leaves idle (C2: 64 workgroups on 256 CUs).  The
 results of batch i come back in one copy of a packed buffer behind its decode
-(an event wait).  Every step does all of its work inside the timed region.
+(an event wait), read on the host once the D-1 younger batches are queued.
+Every step does all of its work inside the timed region.
 
 Default workload = BASELINE.json configs[1] (C2): B=64 utterances per GPU,
 T=500 frames, hidden 256, vocab 29, beam 50 (--config C3/C4/C5/BL select the
@@ -39,6 +46,12 @@ import time
 from pathlib import Path
 
 import numpy as np
+
+# One hardware queue per HIP stream: D decode streams + the recurrence and
+# GEMM streams of production exceed HIP's default of 4, and streams sharing a
+# queue run one after another (C5 with 5 streams on 4 queues: 1.03 M vs
+# 3.48 M frames/s, gpurun_out/r2g31).  Read when the HIP runtime starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 try:
     import torch
@@ -223,7 +236,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=None,
@@ -246,6 +259,11 @@ def main():
                     help="batches decoded concurrently, each on its own HIP stream and CU group "
                          "(0 = auto: as many one-CU-per-utterance groups as fit beside production, "
                          "at most 3; 1 = one decode at a time)")
+    ap.add_argument("--prod-split", default="auto", choices=["auto", "off", "prod", "all"],
+                    help="production on two streams: the recurrence on the production CUs, the "
+                         "input/emission GEMMs on a second stream (prod: the same CUs, all: every CU) "
+                         "issued one batch ahead, so batch i+2's input projection overlaps batch "
+                         "i+1's recurrence (auto: all when D > 1 and H <= 256)")
     ap.add_argument("--result-stream", action="store_true",
                     help="run each batch's traceback on a third stream (measured slower at C2)")
     ap.add_argument("--overlap-results", action="store_true",
@@ -330,21 +348,55 @@ def main():
                       "groups": f"; {D} batches decoding at once, batch i on stream i % {D} restricted to "
                                 f"CUs [{gcu}*(i % {D}), {gcu}*(i % {D} + 1)) (one per utterance), "
                                 f"production on CUs [{D * gcu}, {ncu})"}[split]
+        psplit = args.prod_split
+        if psplit == "auto":   # C2 (r2g34): off 46.4, prod 49.4, all 58.6 M frames/s;
+            # C5 (H = 1024, 2000 recurrence launches): a split is slower
+            psplit = "all" if D > 1 and H <= 256 else "off"
+        if psplit == "off":
+            s_gemm = s_prod
+        elif psplit == "all":
+            s_gemm = torch.cuda.Stream()
+        else:   # a second stream on the production CUs
+            s_gemm = cu_range_stream(D * gcu if D > 1 else 0, ncu) if split == "groups" else torch.cuda.Stream()
+        if psplit != "off":
+            split_note += (f"; production split: recurrence on its stream, input/emission GEMMs on a "
+                           f"second stream ({'production CUs' if psplit == 'prod' else 'all CUs'}) one "
+                           f"batch ahead")
         if args.result_stream:   # tracebacks off the decode stream
             s_res = torch.cuda.Stream()
             for d in decs:
                 d.set_result_stream(s_res.cuda_stream)
         ev_ready = [torch.cuda.Event() for _ in range(nbuf)]
         ev_free = [torch.cuda.Event() for _ in range(nbuf)]
+        ev_proj = [torch.cuda.Event() for _ in range(nbuf)]
+        ev_rec = [torch.cuda.Event() for _ in range(nbuf)]
         prod_stream = s_prod.cuda_stream
     else:
         prod_stream = 0
         split_note = ""
+        psplit = "off"
 
     def produce(k, x=d_x, nb=B):
         """RNN forward + emission projection of a batch into buffer k."""
         asr.rnn_fwd(x, d_wih, d_whh, d_bih, d_bhh, d_hid[k], T, nb, stream=prod_stream)
         asr.linear_fwd(d_hid[k], d_wout, d_bout, d_emis[k], asr.EPI_BIAS_LOGSOFTMAX, prod_stream)
+
+    def produce_head(k):
+        """Split production, part 1: input projection of buffer k's batch on the
+        GEMM stream, then its recurrence on the recurrence stream."""
+        asr.linear_fwd(d_x, d_wih, None, d_hid[k], asr.EPI_NONE, s_gemm.cuda_stream)
+        ev_proj[k].record(s_gemm)
+        s_prod.wait_event(ev_proj[k])
+        asr.rnn_recur_fwd(d_whh, d_bih, d_bhh, d_hid[k], T, B, stream=prod_stream)
+        ev_rec[k].record(s_prod)
+
+    def produce_tail(k):
+        """Split production, part 2: emission projection of buffer k once its
+        recurrence is done and its previous batch's decode has finished."""
+        s_gemm.wait_event(ev_rec[k])
+        s_gemm.wait_event(ev_free[k])
+        asr.linear_fwd(d_hid[k], d_wout, d_bout, d_emis[k], asr.EPI_BIAS_LOGSOFTMAX, s_gemm.cuda_stream)
+        ev_ready[k].record(s_gemm)
 
     if args.decode_only:   # emissions computed once, outside the timed region
         produce(0)
@@ -373,10 +425,17 @@ def main():
                 enqueue(0)
                 collect(0)
             return
-        with torch.cuda.stream(s_prod):
-            produce(0)
-            ev_ready[0].record(s_prod)
         lag = D - 1 if D > 1 else (1 if args.overlap_results else 0)
+        split_prod = psplit != "off"
+        if split_prod:
+            produce_head(0)
+            produce_tail(0)
+            if n > 1:
+                produce_head(1 % nbuf)
+        else:
+            with torch.cuda.stream(s_prod):
+                produce(0)
+                ev_ready[0].record(s_prod)
         pending = []   # buffers decoded, results not read yet (oldest first)
         for i in range(n):
             k = i % nbuf
@@ -388,7 +447,15 @@ def main():
             enqueue(k, sd.cuda_stream)
             ev_free[k].record(sd)
             pending.append(k)
-            if i + 1 < n:   # batch i+1 is produced while batch i is decoded
+            if split_prod:
+                # GEMM stream order: batch i+2's input projection, then batch
+                # i+1's emission projection (which waits for i+1's recurrence),
+                # so the projection overlaps the recurrence of batch i+1
+                if i + 2 < n:
+                    produce_head((i + 2) % nbuf)
+                if i + 1 < n:
+                    produce_tail((i + 1) % nbuf)
+            elif i + 1 < n:   # batch i+1 is produced while batch i is decoded
                 kn = (i + 1) % nbuf
                 s_prod.wait_event(ev_free[kn])
                 produce(kn)
@@ -563,6 +630,22 @@ def cu_group_streams(D, gcu, ncu):
         _RAW_STREAMS.append((hip, st.value))
         out.append(torch.cuda.ExternalStream(st.value))
     return out[-1], out[:-1]
+
+
+def cu_range_stream(lo, hi):
+    """One HIP stream restricted to CUs [lo, hi), as a torch external stream."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    words = (ncu + 31) // 32
+    m = [0] * words
+    for cu in range(lo, hi):
+        m[cu // 32] |= 1 << (cu % 32)
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), (ctypes.c_uint32 * words)(*m))
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+    _RAW_STREAMS.append((hip, st.value))
+    return torch.cuda.ExternalStream(st.value)
 
 
 _RAW_STREAMS = []

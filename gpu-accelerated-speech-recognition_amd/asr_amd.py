@@ -48,7 +48,7 @@ EXPORTS = [
     "asr_host_free", "asr_memcpy_h2d", "asr_memcpy_d2h", "asr_memcpy_d2d", "asr_memset",
     "asr_stream_create", "asr_stream_destroy", "asr_stream_sync", "asr_device_sync",
     "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
-    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
+    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_recur_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
     "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
@@ -104,6 +104,7 @@ def lib() -> ctypes.CDLL:
         "asr_linear_fwd": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_cell_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
+        "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -229,6 +230,16 @@ def rnn_fwd(x: DeviceMatrix, W_ih: DeviceMatrix, W_hh: DeviceMatrix, b_ih: Devic
     inp, H = W_ih.rows, W_ih.cols
     check(lib().asr_rnn_fwd(x.ptr, h0.ptr if h0 else None, W_ih.ptr, W_hh.ptr, b_ih.ptr,
                             b_hh.ptr, hid.ptr, T, B, inp, H, stream), "asr_rnn_fwd")
+    return hid
+
+
+def rnn_recur_fwd(W_hh: DeviceMatrix, b_ih: DeviceMatrix, b_hh: DeviceMatrix, hid: DeviceMatrix,
+                  T: int, B: int, h0: Optional[DeviceMatrix] = None, stream: int = 0) -> DeviceMatrix:
+    """The recurrence stage alone (asr_rnn_recur_fwd): hid holds x.W_ih on entry,
+    the hidden states on return."""
+    H = W_hh.cols
+    check(lib().asr_rnn_recur_fwd(h0.ptr if h0 else None, W_hh.ptr, b_ih.ptr, b_hh.ptr, hid.ptr,
+                                  T, B, H, stream), "asr_rnn_recur_fwd")
     return hid
 
 

@@ -216,6 +216,12 @@ int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float*
     return rnn_recurrence(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
 }
 
+int asr_rnn_recur_fwd(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
+                      float* hid, int T, int B, int H, asr_stream_t s) {
+    if (!W_hh || !b_ih || !b_hh || !hid || T <= 0 || B <= 0 || H <= 0) return ASR_ERR_ARG;
+    return rnn_recurrence(h0, W_hh, b_ih, b_hh, hid, T, B, H, asr_stream(s));
+}
+
 size_t asr_rnn_bidir_workspace_bytes(int T, int B, int H) {
     if (T <= 0 || B <= 0 || H <= 0) return 0;
     return 2 * (size_t)T * B * H * sizeof(float);

@@ -113,6 +113,15 @@ int asr_rnn_fwd(const float* d_x, const float* d_h0, const float* d_W_ih, const 
                 const float* d_b_ih, const float* d_b_hh, float* d_hiddens, int T, int B,
                 int in, int H, asr_stream_t s);
 
+/* The recurrence stage of asr_rnn_fwd alone, for callers that run the input
+ * projection themselves (e.g. asr_linear_fwd(x, W_ih, NULL, hiddens, ...,
+ * ASR_EPI_NONE) on another stream, so that the next batch's projection
+ * overlaps this batch's recurrence): on entry d_hiddens [T*B, H] holds
+ * P = x.W_ih, on return the hidden states, in place.  asr_rnn_fwd is exactly
+ * this after that GEMM (RNN.cu:9-30 split at its two stages). */
+int asr_rnn_recur_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_ih,
+                      const float* d_b_hh, float* d_hiddens, int T, int B, int H, asr_stream_t s);
+
 /* Bidirectional single-layer RNN — nn.RNN(bidirectional=True) of the Python
  * baseline (baseline/model.py:30, "bidir true"); the C++
  * RNN class (RNN.h:13-20) has no such mode, so this is an added entry point.

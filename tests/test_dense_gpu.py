@@ -152,6 +152,31 @@ def test_rnn_forward(T, B, I, H):
     close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 5e-5)
 
 
+@pytest.mark.parametrize("T,B,I,H", [(50, 64, 256, 256), (12, 4, 24, 300)])
+def test_rnn_recur_stage_equals_rnn_fwd(T, B, I, H):
+    """asr_linear_fwd(x, W_ih, EPI_NONE) + asr_rnn_recur_fwd on two streams is
+    asr_rnn_fwd bit for bit (the bench's split production)."""
+    rng = np.random.default_rng(T + H)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih, w_hh = dm(rng.uniform(-s, s, (I, H)).astype(np.float32)), dm(rng.uniform(-s, s, (H, H)).astype(np.float32))
+    b_ih = dm(rng.uniform(-0.1, 0.1, (H, 1)).astype(np.float32))
+    b_hh = dm(rng.uniform(-0.1, 0.1, (H, 1)).astype(np.float32))
+    h0 = dm(rng.uniform(-1, 1, (B, H)).astype(np.float32))
+    ref, hid = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dm(x), w_ih, w_hh, b_ih, b_hh, ref, T, B, h0=h0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    asr.linear_fwd(dm(x), w_ih, None, hid, asr.EPI_NONE, s1.cuda_stream)
+    ev = torch.cuda.Event()
+    ev.record(s1)
+    s2.wait_event(ev)
+    asr.rnn_recur_fwd(w_hh, b_ih, b_hh, hid, T, B, h0=h0, stream=s2.cuda_stream)
+    s2.synchronize()
+    assert np.array_equal(hid.toCpu(), ref.toCpu())
+    with pytest.raises(Exception):
+        asr.rnn_recur_fwd(w_hh, b_ih, b_hh, hid, 0, B)
+
+
 def test_rnn_cell_forward():
     rng = np.random.default_rng(5)
     B, I, H = 17, 33, 70
