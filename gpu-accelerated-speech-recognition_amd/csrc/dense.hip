@@ -254,6 +254,16 @@ int gemm_launch(const GemmArgs& g, int epi, hipStream_t s) {
 // read from HBM once per utterance instead of once per step.  h_{t-1} is
 // broadcast from LDS as [quarter][68] (conflict-free ds_read_b128).
 // ---------------------------------------------------------------------------
+// Workgroup barrier ordering LDS only: the step's global store of h_t (and
+// the prefetch of P_{t+1}) stay in flight across it.  __syncthreads() orders
+// global memory too, so every step waited for its store to reach memory
+// (s_waitcnt vmcnt(0) before each s_barrier).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 constexpr int RNN_HMAX = 256;
 constexpr int RNN_QS = 68;   // LDS stride of one quarter (floats)
 
@@ -283,14 +293,25 @@ __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict
     const float bias = col ? (b_hh[j] + b_ih[j]) : 0.f;
     const int jq = col ? j / KQ : 0, ji = col ? j - jq * KQ : 0;
     const bool writer = col && q == 0;
-    float* prow = hid + (long)b * H + j;     // P_t / h_t at prow[t*B*H]
+    // P_t / h_t of this utterance's column j at hid[t*B*H + b*H + j], through
+    // one buffer resource per step (base uniform, B*H*4 bytes): lanes other
+    // than the column's writer get an out-of-range offset, so their loads
+    // return 0 and their stores are dropped.  No branch around the memory
+    // ops, so the wait before each step only covers the prefetch of P_{t+1},
+    // never the store of h_t.
     const long tstride = (long)B * H;
-    float pnext = writer ? prow[0] : 0.f;
+    const int nbytes = (int)(tstride * 4);
+    const int voff = writer ? (b * H + j) * 4 : 0x7ffffff0;
+    constexpr int RSRC3 = 0x00020000;   // gfx9 buffer descriptor word 3 (raw 32-bit data)
+    float pnext = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        __builtin_amdgcn_make_buffer_rsrc(hid, 0, nbytes, RSRC3), voff, 0, 0));
     __syncthreads();
     int cur = 0;
     for (int t = 0; t < T; t++) {
         const float p = pnext;
-        if (writer && t + 1 < T) pnext = prow[(t + 1) * tstride];
+        float* base = hid + t * tstride;
+        pnext = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            __builtin_amdgcn_make_buffer_rsrc(base + tstride, 0, t + 1 < T ? nbytes : 0, RSRC3), voff, 0, 0));
         const float4* hq = reinterpret_cast<const float4*>(&hs[cur][q * RNN_QS]);
         float acc = 0.f;
 #pragma unroll
@@ -303,19 +324,20 @@ __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict
         }
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
-        if (writer) {
-            const float h = tanhf((p + acc) + bias);
-            hs[cur ^ 1][jq * RNN_QS + ji] = h;
-            prow[t * tstride] = h;
-        }
+        const float h = tanhf((p + acc) + bias);
+        if (writer) hs[cur ^ 1][jq * RNN_QS + ji] = h;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h),
+                                              __builtin_amdgcn_make_buffer_rsrc(base, 0, nbytes, RSRC3),
+                                              voff, 0, 0);
         cur ^= 1;
-        __syncthreads();
+        lds_barrier();
     }
 }
 
 int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                      float* hid, int T, int B, int H, hipStream_t s) {
     if (H > RNN_HMAX) return ASR_ERR_UNSUPPORTED;
+    if ((long)B * H * 4 > 0x7fffffe0L) return ASR_ERR_UNSUPPORTED;   // one step's rows per buffer resource
     hipLaunchKernelGGL(rnn_recur_kernel, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid,
                        T, B, H);
     ASR_LAUNCH_TRY();
