@@ -116,24 +116,12 @@ __device__ __forceinline__ void mma_tile(Tile<BN, BK>& L, const float* __restric
     }
 }
 
-// C/D layout of 16x16 MFMA tiles (dtype-independent on gfx950):
-// element j of lane l is row (l>>4)*4 + j, column l & 15.
-template <int BN, int BK, int EPI, int VEC>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
-    __shared__ Tile<BN, BK> L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-    f32x4 acc[BN / 16], acc2[BN / 16];
-#pragma unroll
-    for (int nt = 0; nt < BN / 16; nt++) {
-        acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    mma_tile<BN, BK, VEC>(L, g.A, g.B, g.M, g.N, g.K, g.sam, g.sak, g.sbk, g.sbn, m0, n0, acc);
-    if (EPI == EPI_DUAL_TANH)
-        mma_tile<BN, BK, VEC>(L, g.A2, g.B2, g.M, g.N, g.K2, g.K2, 1, g.N, 1, m0, n0, acc2);
-
-    const int rbase = m0 + w * 16 + (lane >> 4) * 4;
+// Epilogue of a 16-row x BN tile held in 16x16 MFMA C fragments: rows
+// rbase + j (j < 4) of lane group lane >> 4, columns n0 + nt*16 + (lane & 15).
+template <int BN, int EPI>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, const f32x4 (&acc)[BN / 16],
+                                              const f32x4 (&acc2)[BN / 16], int rbase, int n0,
+                                              int lane) {
     if (EPI == EPI_LOGSOFTMAX) {
         // Whole row in this workgroup (N <= BN): row r = rbase + j lives in
         // the 16 lanes of group lane>>4, across the BN/16 tiles.
@@ -190,6 +178,108 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     }
 }
 
+// C/D layout of 16x16 MFMA tiles (dtype-independent on gfx950):
+// element j of lane l is row (l>>4)*4 + j, column l & 15.
+template <int BN, int BK, int EPI, int VEC>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+    __shared__ Tile<BN, BK> L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    f32x4 acc[BN / 16], acc2[BN / 16];
+#pragma unroll
+    for (int nt = 0; nt < BN / 16; nt++) {
+        acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    mma_tile<BN, BK, VEC>(L, g.A, g.B, g.M, g.N, g.K, g.sam, g.sak, g.sbk, g.sbn, m0, n0, acc);
+    if (EPI == EPI_DUAL_TANH)
+        mma_tile<BN, BK, VEC>(L, g.A2, g.B2, g.M, g.N, g.K2, g.K2, 1, g.N, 1, m0, n0, acc2);
+
+    gemm_epilogue<BN, EPI>(g, acc, acc2, m0 + w * 16 + (lane >> 4) * 4, n0, lane);
+}
+
+// Narrow outputs (N <= 64: the emission projection, V = 29 / 47): a stream of
+// A with nothing of it in LDS.  Each wave owns 16 rows; lane (r, g) = (lane &
+// 15, lane >> 4) loads row r's float4 at k = 16i + 4g of a 256-deep chunk,
+// all 16 at once (16 KB per wave in flight), and feeds element e of float4 i
+// as the A fragment of MFMA step (i, e): the step's four k-slots are then
+// k = 16i + 4g + e, g = 0..3 — any k order is the same sum.  B (K x N, tiny)
+// is staged transposed in LDS per chunk so that the matching B fragment is one
+// ds_read_b128.
+// Waves per workgroup: 4 at N <= 32 (C2 14.8 us vs 15.1 at 8), 8 at N <= 64
+// (BL, K = 2048: 223 us vs 315 at 4: B is staged per 256-deep chunk).
+constexpr int NS_KC = 256;   // K per chunk
+template <int BN, int EPI, int NS_W = (BN <= 32 ? 4 : 8)>
+__global__ __launch_bounds__(64 * NS_W) void gemm_narrow_kernel(GemmArgs g) {
+    constexpr int NT = BN / 16;
+    constexpr int BTS = NS_KC + 4;   // B^T row stride (floats), rows 16-B aligned
+    __shared__ __attribute__((aligned(16))) float Bt[BN * BTS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, gq = lane >> 4;
+    const int row = blockIdx.x * (16 * NS_W) + w * 16 + r;
+    const bool rok = row < g.M;
+    const float* arow = g.A + (long)(rok ? row : 0) * g.sam;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < g.K; k0 += NS_KC) {
+        f32x4 a[NS_KC / 16];
+#pragma unroll
+        for (int i = 0; i < NS_KC / 16; i++) {
+            const int k = k0 + 16 * i + 4 * gq;
+            a[i] = (rok && k < g.K) ? *reinterpret_cast<const f32x4*>(arow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (k0 > 0) __syncthreads();   // the previous chunk's B^T is consumed
+        {   // all of the chunk's B loads in flight at once, then the LDS stores
+            constexpr int NBL = BN * NS_KC / (64 * NS_W);
+            float bv[NBL];
+#pragma unroll
+            for (int it = 0; it < NBL; it++) {
+                const int idx = tid + it * 64 * NS_W;
+                const int kk = idx / BN, n = idx - kk * BN, k = k0 + kk;
+                bv[it] = (k < g.K && n < g.N) ? g.B[(long)k * g.sbk + (long)n * g.sbn] : 0.f;
+            }
+#pragma unroll
+            for (int it = 0; it < NBL; it++) {
+                const int idx = tid + it * 64 * NS_W;
+                const int kk = idx / BN, n = idx - kk * BN;
+                Bt[n * BTS + kk] = bv[it];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NS_KC / 16; i++) {
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) {
+                const f32x4 b4 = *reinterpret_cast<const f32x4*>(&Bt[(nt * 16 + r) * BTS + 16 * i + 4 * gq]);
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b4[e], acc[nt], 0, 0, 0);
+            }
+        }
+    }
+    gemm_epilogue<BN, EPI>(g, acc, acc, blockIdx.x * (16 * NS_W) + w * 16 + gq * 4, 0, lane);
+}
+
+template <int EPI>
+static int launch_gemm_narrow(const GemmArgs& g, hipStream_t s) {
+    if (g.N <= 32)
+        hipLaunchKernelGGL((gemm_narrow_kernel<32, EPI>), dim3((g.M + 63) / 64), dim3(256), 0, s, g);
+    else
+        hipLaunchKernelGGL((gemm_narrow_kernel<64, EPI>), dim3((g.M + 127) / 128), dim3(512), 0, s, g);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ASR_GEMM_NARROW=0: the tiled kernel for narrow outputs too (A/B runs).
+static bool narrow_off() {
+    static const bool off = [] {
+        const char* e = getenv("ASR_GEMM_NARROW");
+        return e && e[0] == '0';
+    }();
+    return off;
+}
+
 template <int BN, int BK, int EPI>
 static int launch_gemm_bk(const GemmArgs& g, hipStream_t s) {
     const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
@@ -222,6 +312,9 @@ static int launch_gemm_bn(const GemmArgs& g, hipStream_t s) {
 
 template <int EPI>
 static int launch_gemm_epi(const GemmArgs& g, hipStream_t s) {
+    // the A stream as float4 rows: narrow outputs take the LDS-free A path
+    const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
+    if (EPI != EPI_DUAL_TANH && g.N <= 64 && va && !narrow_off()) return launch_gemm_narrow<EPI>(g, s);
     if (g.N <= 32) return launch_gemm_bn<32, EPI>(g, s);
     return launch_gemm_bn<64, EPI>(g, s);
 }
