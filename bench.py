@@ -51,7 +51,8 @@ import numpy as np
 # GEMM streams of production exceed HIP's default of 4, and streams sharing a
 # queue run one after another (C5 with 5 streams on 4 queues: 1.03 M vs
 # 3.48 M frames/s, gpurun_out/r2g31).  Read when the HIP runtime starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 try:
     import torch
@@ -264,6 +265,15 @@ def main():
                          "input/emission GEMMs on a second stream (prod: the same CUs, all: every CU) "
                          "issued one batch ahead, so batch i+2's input projection overlaps batch "
                          "i+1's recurrence (auto: all when D > 1 and H <= 256)")
+    ap.add_argument("--prod-streams", type=int, default=0,
+                    help="production streams (unsplit production): batch i is produced on stream "
+                         "i %% P, P batches ahead of its decode, so the recurrences of P batches run "
+                         "at once (0 = auto: 2 when D > 1 and H > 256, i.e. C5's latency-bound "
+                         "per-frame recurrence launches; else 1)")
+    ap.add_argument("--graph-production", default="auto", choices=["auto", "on", "off"],
+                    help="capture each buffer's production (RNN + projection: at C5 ~2000 recurrence "
+                         "launches) once in a HIP graph and replay it per batch, so the host no longer "
+                         "queues every launch (auto: on when H > 256 and production is not split)")
     ap.add_argument("--result-stream", action="store_true",
                     help="run each batch's traceback on a third stream (measured slower at C2)")
     ap.add_argument("--overlap-results", action="store_true",
@@ -324,7 +334,12 @@ def main():
     # produced, and a buffer is only produced into after its batch's results
     # were read (asr_amd.h lifetime rule: an overflow retry re-reads it), so
     # D + 1 buffers (--overlap-results, D = 1: a third one).
-    nbuf = (D + 1 if D > 1 else (3 if args.overlap_results else 2)) if pipeline else 1
+    split_prod_auto = D > 1 and H <= 256   # --prod-split auto (below)
+    Pn = 1
+    if pipeline and not (args.prod_split in ("prod", "all") or (args.prod_split == "auto" and split_prod_auto)):
+        Pn = args.prod_streams or (2 if D > 1 and H > 256 else 1)
+    # P production streams produce P batches ahead: D + P buffers
+    nbuf = (D + Pn if D > 1 or Pn > 1 else (3 if args.overlap_results else 2)) if pipeline else 1
     d_hid = [asr.DeviceMatrix(T * B, H) for _ in range(nbuf)]
     d_emis = [asr.DeviceMatrix(T * B, V) for _ in range(nbuf)]
     decs = [asr.CTCDecoder(V, beam, 0, waves=args.waves) for _ in range(nbuf)]
@@ -351,7 +366,7 @@ def main():
         psplit = args.prod_split
         if psplit == "auto":   # C2 (r2g34): off 46.4, prod 49.4, all 58.6 M frames/s;
             # C5 (H = 1024, 2000 recurrence launches): a split is slower
-            psplit = "all" if D > 1 and H <= 256 else "off"
+            psplit = "all" if split_prod_auto else "off"
         if psplit == "off":
             s_gemm = s_prod
         elif psplit == "all":
@@ -362,6 +377,11 @@ def main():
             split_note += (f"; production split: recurrence on its stream, input/emission GEMMs on a "
                            f"second stream ({'production CUs' if psplit == 'prod' else 'all CUs'}) one "
                            f"batch ahead")
+        s_prods = [s_prod]
+        for _ in range(Pn - 1):   # more production streams on the production CUs
+            s_prods.append(cu_range_stream(D * gcu, ncu) if split == "groups" else torch.cuda.Stream())
+        if Pn > 1:
+            split_note += f"; {Pn} production streams, batch i produced on stream i % {Pn}"
         if args.result_stream:   # tracebacks off the decode stream
             s_res = torch.cuda.Stream()
             for d in decs:
@@ -376,10 +396,11 @@ def main():
         split_note = ""
         psplit = "off"
 
-    def produce(k, x=d_x, nb=B):
+    def produce(k, x=d_x, nb=B, stream=None):
         """RNN forward + emission projection of a batch into buffer k."""
-        asr.rnn_fwd(x, d_wih, d_whh, d_bih, d_bhh, d_hid[k], T, nb, stream=prod_stream)
-        asr.linear_fwd(d_hid[k], d_wout, d_bout, d_emis[k], asr.EPI_BIAS_LOGSOFTMAX, prod_stream)
+        st = prod_stream if stream is None else stream
+        asr.rnn_fwd(x, d_wih, d_whh, d_bih, d_bhh, d_hid[k], T, nb, stream=st)
+        asr.linear_fwd(d_hid[k], d_wout, d_bout, d_emis[k], asr.EPI_BIAS_LOGSOFTMAX, st)
 
     def produce_head(k):
         """Split production, part 1: input projection of buffer k's batch on the
@@ -432,10 +453,10 @@ def main():
             produce_tail(0)
             if n > 1:
                 produce_head(1 % nbuf)
-        else:
-            with torch.cuda.stream(s_prod):
-                produce(0)
-                ev_ready[0].record(s_prod)
+        else:   # the first P batches, one per production stream
+            for j in range(min(Pn, n)):
+                produce(j % nbuf, stream=s_prods[j % Pn].cuda_stream)
+                ev_ready[j % nbuf].record(s_prods[j % Pn])
         pending = []   # buffers decoded, results not read yet (oldest first)
         for i in range(n):
             k = i % nbuf
@@ -455,16 +476,46 @@ def main():
                     produce_head((i + 2) % nbuf)
                 if i + 1 < n:
                     produce_tail((i + 1) % nbuf)
-            elif i + 1 < n:   # batch i+1 is produced while batch i is decoded
-                kn = (i + 1) % nbuf
-                s_prod.wait_event(ev_free[kn])
-                produce(kn)
-                ev_ready[kn].record(s_prod)
+            elif i + Pn < n:   # batch i+P is produced while batch i is decoded
+                kn = (i + Pn) % nbuf
+                sp = s_prods[(i + Pn) % Pn]
+                sp.wait_event(ev_free[kn])
+                produce(kn, stream=sp.cuda_stream)
+                ev_ready[kn].record(sp)
             # read the oldest batch once `lag` newer ones are decoding behind it
             while len(pending) > lag:
                 collect(pending.pop(0))
         while pending:
             collect(pending.pop(0))
+
+    graphs = None
+    if pipeline and psplit == "off" and (args.graph_production == "on" or
+                                         (args.graph_production == "auto" and H > 256)):
+        # one HIP graph per buffer (fixed pointers), captured after a first
+        # eager production sized every workspace; replayed on the production
+        # streams by produce_graph()
+        produce(0)
+        asr.synchronize()
+        s_cap = torch.cuda.Stream()
+        graphs = []
+        for k in range(nbuf):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s_cap):
+                produce(k, stream=s_cap.cuda_stream)
+            graphs.append(g)
+        asr.synchronize()
+        split_note += "; each batch's production replayed from a HIP graph"
+
+    if graphs is not None:
+        eager_produce = produce
+
+        def produce(k, x=d_x, nb=B, stream=None):   # noqa: F811
+            """Replay buffer k's captured production on `stream`."""
+            if x is not d_x or nb != B:
+                return eager_produce(k, x, nb, stream)
+            sp = next((t for t in s_prods if t.cuda_stream == stream), s_prod) if stream is not None else s_prod
+            with torch.cuda.stream(sp):
+                graphs[k].replay()
 
     if pipeline:
         # every buffer's decoder handle sizes its workspace (hipMalloc, which
@@ -561,7 +612,7 @@ def main():
                        f": B={B}/GPU (global {GB}), T={T}, hidden={H}, vocab={V}, beam={beam}",
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
-                       "inflight_decodes": D,
+                       "inflight_decodes": D, "production_streams": Pn,
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
                                     "on another" + split_note +
                                     ("; tracebacks on a third stream" if args.result_stream else "")
