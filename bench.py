@@ -526,6 +526,9 @@ def main():
             asr.synchronize()
             enqueue(k, s_decs[k % D].cuda_stream)
             collect(k)
+        # and one pipelined pass over every buffer, stream and event (torch
+        # creates an event's HIP event at its first record)
+        run(nbuf + Pn)
         kernel_ms.clear()
     run(args.warmup)
     kernel_ms.clear()
