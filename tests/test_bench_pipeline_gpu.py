@@ -1,0 +1,39 @@
+"""bench.py's pipelines decode the same hypotheses: D batches in flight on
+disjoint CU groups, the production split over two streams, HIP-graph
+production replays and the sequential loop all gather the same digest
+(labels + fp64 log-probs of every utterance) — the scheduling changes when
+work runs, never what it computes.  Each bench run is one subprocess (a few
+seconds at T = 100), run one after another."""
+import json
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _bench(*args):
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", "--steps", "6", "--warmup", "2",
+           "--T", "100", *args]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    return line
+
+
+def test_inflight_and_split_production_match_sequential():
+    seq = _bench("--no-pipeline")
+    runs = {
+        "d1": _bench("--inflight", "1"),
+        "d3_split_all": _bench("--inflight", "3"),              # auto: production split, GEMMs on all CUs
+        "d2_unsplit_graph": _bench("--inflight", "2", "--prod-split", "off", "--graph-production", "on",
+                                   "--prod-streams", "2"),
+    }
+    assert seq["gather"]["utterances"] == 64
+    for name, r in runs.items():
+        assert r["gather"] == seq["gather"], name
+    assert runs["d3_split_all"]["config"]["inflight_decodes"] == 3
+    assert runs["d2_unsplit_graph"]["config"]["production_streams"] == 2
