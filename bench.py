@@ -260,9 +260,16 @@ def main():
                     help="batches decoded concurrently, each on its own HIP stream and CU group "
                          "(0 = auto: as many one-CU-per-utterance groups as fit beside production, "
                          "at most 3; 1 = one decode at a time)")
-    ap.add_argument("--prod-split", default="auto", choices=["auto", "off", "prod", "all"],
+    ap.add_argument("--decode-cus", type=int, default=0,
+                    help="CUs per decode group (0: one per utterance, B rounded up to 8); fewer "
+                         "CUs than utterances puts several decode workgroups on a CU when their "
+                         "registers allow (--waves 4: 188 VGPRs, one wave per SIMD each)")
+    ap.add_argument("--packed", action="store_true",
+                    help="4-wave decode workgroups two to a CU, 5 batches in flight (C2-like shapes)")
+    ap.add_argument("--prod-split", default="auto", choices=["auto", "off", "prod", "all", "norec"],
                     help="production on two streams: the recurrence on the production CUs, the "
-                         "input/emission GEMMs on a second stream (prod: the same CUs, all: every CU) "
+                         "input/emission GEMMs on a second stream (prod: the same CUs, all: every CU, "
+                         "norec: every CU but the recurrence's, which then get exactly one per utterance) "
                          "issued one batch ahead, so batch i+2's input projection overlaps batch "
                          "i+1's recurrence (auto: all when D > 1 and H <= 256)")
     ap.add_argument("--prod-streams", type=int, default=0,
@@ -320,14 +327,27 @@ def main():
     d_x = DM(make_features(T, B, In, first))
     pipeline = not args.no_pipeline and not args.decode_only
     ncu = torch.cuda.get_device_properties(local).multi_processor_count if torch is not None else 256
-    gcu = min(ncu, -(-B // 8) * 8)   # one decode workgroup per utterance, one per CU
+    bcu = -(-B // 8) * 8   # CUs of one workgroup per utterance
+    # --packed (C2-like shapes: H <= 256, V <= 63, a batch on at most a
+    # quarter of the CUs): 4-wave decode workgroups (188 VGPRs, one wave per
+    # SIMD) two to a CU, so a batch's decode group is half as many CUs; 1.72 ->
+    # 1.89 ms per decode, 5 groups in flight: 64.5 M vs 58.8 M frames/s at 100
+    # steps (r2g49), but its first timed run after a short warmup pays ~10 ms
+    # once (20 steps / warmup 5: 27-28 M; r2g50/51, cause not found), so it is
+    # not the default.
+    packed = (args.packed and pipeline and not args.waves and not args.decode_cus and not args.inflight
+              and H <= 256 and V + 1 <= 64 and 4 * bcu <= ncu)
+    waves = 4 if packed else args.waves
+    gcu = min(ncu, args.decode_cus or (-(-B // 16) * 8 if packed else bcu))
     D = 1
     if pipeline:
         # auto: up to 3 decode groups for H <= 256 (C2: 38.7 M vs 21.1 M frames/s at
         # D = 1), 2 for the H = 1024 recurrence (C5: D = 2 3.48 M, D = 3 2.99 M,
-        # gpurun_out/r2g31); one HIP stream per group plus production stays
-        # within the box's 4 hardware queues (D = 4 at C5: 1.03 M, serialised)
-        D = args.inflight or max(1, min(3 if H <= 256 else 2, ncu // gcu - 1))
+        # gpurun_out/r2g31); packed: 5 (one recurrence group of bcu CUs beside them)
+        if packed:
+            D = max(1, min(5, (ncu - bcu) // gcu))
+        else:
+            D = args.inflight or max(1, min(3 if H <= 256 else 2, ncu // gcu - 1))
         if D > 1 and (D + 1) * gcu > ncu:
             raise SystemExit(f"--inflight {D}: {D} decode groups of {gcu} CUs + production exceed {ncu} CUs")
     # Buffer i % nbuf holds batch i.  D batches are decoding while batch i+1 is
@@ -336,13 +356,14 @@ def main():
     # D + 1 buffers (--overlap-results, D = 1: a third one).
     split_prod_auto = D > 1 and H <= 256   # --prod-split auto (below)
     Pn = 1
-    if pipeline and not (args.prod_split in ("prod", "all") or (args.prod_split == "auto" and split_prod_auto)):
+    if pipeline and not (args.prod_split in ("prod", "all", "norec") or
+                         (args.prod_split == "auto" and split_prod_auto)):
         Pn = args.prod_streams or (2 if D > 1 and H > 256 else 1)
     # P production streams produce P batches ahead: D + P buffers
     nbuf = (D + Pn if D > 1 or Pn > 1 else (3 if args.overlap_results else 2)) if pipeline else 1
     d_hid = [asr.DeviceMatrix(T * B, H) for _ in range(nbuf)]
     d_emis = [asr.DeviceMatrix(T * B, V) for _ in range(nbuf)]
-    decs = [asr.CTCDecoder(V, beam, 0, waves=args.waves) for _ in range(nbuf)]
+    decs = [asr.CTCDecoder(V, beam, 0, waves=waves) for _ in range(nbuf)]
     if pipeline:   # HIP streams/events via torch (same HIP runtime as libasr_amd)
         torch.cuda.set_device(local)
         s_prod, s_dec = torch.cuda.Stream(), torch.cuda.Stream()
@@ -366,17 +387,25 @@ def main():
         psplit = args.prod_split
         if psplit == "auto":   # C2 (r2g34): off 46.4, prod 49.4, all 58.6 M frames/s;
             # C5 (H = 1024, 2000 recurrence launches): a split is slower
-            psplit = "all" if split_prod_auto else "off"
+            psplit = ("norec" if packed else "all") if split_prod_auto else "off"
         if psplit == "off":
             s_gemm = s_prod
         elif psplit == "all":
             s_gemm = torch.cuda.Stream()
+        elif psplit == "norec" and split == "groups":
+            # recurrence on the B CUs after the decode groups (one workgroup per
+            # utterance); the GEMMs on every other CU, decode groups included
+            r0, r1 = D * gcu, min(ncu, D * gcu + -(-B // 8) * 8)
+            s_prod = cu_range_stream(r0, r1)
+            s_gemm = cu_ranges_stream([(0, r0), (r1, ncu)])
+            split_note = split_note.replace(f"production on CUs [{D * gcu}, {ncu})",
+                                            f"recurrence on CUs [{r0}, {r1})")
         else:   # a second stream on the production CUs
             s_gemm = cu_range_stream(D * gcu if D > 1 else 0, ncu) if split == "groups" else torch.cuda.Stream()
         if psplit != "off":
+            where = {"prod": "production CUs", "all": "all CUs", "norec": "all CUs but the recurrence's"}[psplit]
             split_note += (f"; production split: recurrence on its stream, input/emission GEMMs on a "
-                           f"second stream ({'production CUs' if psplit == 'prod' else 'all CUs'}) one "
-                           f"batch ahead")
+                           f"second stream ({where}) one batch ahead")
         s_prods = [s_prod]
         for _ in range(Pn - 1):   # more production streams on the production CUs
             s_prods.append(cu_range_stream(D * gcu, ncu) if split == "groups" else torch.cuda.Stream())
@@ -539,6 +568,13 @@ def main():
     run(args.steps)
     asr.synchronize()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("ASR_BENCH_REPEAT"):   # diagnostics: the same timed run again, to stderr
+        for _ in range(int(os.environ["ASR_BENCH_REPEAT"])):
+            asr.synchronize()
+            t1 = time.perf_counter()
+            run(args.steps)
+            asr.synchronize()
+            print(f"repeat: {1e3 * (time.perf_counter() - t1) / args.steps:.4f} ms/step", file=sys.stderr)
     elapsed = reduce_max_over_ranks(elapsed, world)
     if world > 1:
         dist.barrier()
@@ -615,7 +651,8 @@ def main():
                        f": B={B}/GPU (global {GB}), T={T}, hidden={H}, vocab={V}, beam={beam}",
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
-                       "inflight_decodes": D, "production_streams": Pn,
+                       "inflight_decodes": D, "production_streams": Pn, "decode_waves": waves or 8,
+                       "decode_cus_per_batch": gcu if pipeline and D > 1 else None,
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
                                     "on another" + split_note +
                                     ("; tracebacks on a third stream" if args.result_stream else "")
@@ -688,12 +725,18 @@ def cu_group_streams(D, gcu, ncu):
 
 def cu_range_stream(lo, hi):
     """One HIP stream restricted to CUs [lo, hi), as a torch external stream."""
+    return cu_ranges_stream([(lo, hi)])
+
+
+def cu_ranges_stream(ranges):
+    """One HIP stream restricted to the union of CU ranges [lo, hi)."""
     hip = ctypes.CDLL("libamdhip64.so")
     ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     words = (ncu + 31) // 32
     m = [0] * words
-    for cu in range(lo, hi):
-        m[cu // 32] |= 1 << (cu % 32)
+    for lo, hi in ranges:
+        for cu in range(lo, hi):
+            m[cu // 32] |= 1 << (cu % 32)
     st = ctypes.c_void_p()
     rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), (ctypes.c_uint32 * words)(*m))
     if rc != 0:

@@ -1,5 +1,6 @@
 """bench.py's pipelines decode the same hypotheses: D batches in flight on
-disjoint CU groups, the production split over two streams, HIP-graph
+disjoint CU groups (8-wave decode workgroups one per CU, or 4-wave ones two
+to a CU), the production split over two streams, HIP-graph
 production replays and the sequential loop all gather the same digest
 (labels + fp64 log-probs of every utterance) — the scheduling changes when
 work runs, never what it computes.  Each bench run is one subprocess (a few
@@ -27,6 +28,7 @@ def _bench(*args):
 def test_inflight_and_split_production_match_sequential():
     seq = _bench("--no-pipeline")
     runs = {
+        "packed": _bench("--packed"),   # 4-wave decode workgroups two to a CU, 5 batches in flight
         "d1": _bench("--inflight", "1"),
         "d3_split_all": _bench("--inflight", "3"),              # auto: production split, GEMMs on all CUs
         "d2_unsplit_graph": _bench("--inflight", "2", "--prod-split", "off", "--graph-production", "on",
@@ -36,4 +38,5 @@ def test_inflight_and_split_production_match_sequential():
     for name, r in runs.items():
         assert r["gather"] == seq["gather"], name
     assert runs["d3_split_all"]["config"]["inflight_decodes"] == 3
+    assert runs["packed"]["config"]["decode_waves"] == 4 and runs["packed"]["config"]["inflight_decodes"] == 5
     assert runs["d2_unsplit_graph"]["config"]["production_streams"] == 2
