@@ -38,6 +38,7 @@ checked bit for bit against a 1-GPU decode of the same utterance ids on rank
 """
 import argparse
 import ctypes
+import gc
 import hashlib
 import json
 import os
@@ -563,11 +564,16 @@ def main():
     kernel_ms.clear()
     if world > 1:
         dist.barrier()
+    # no Python garbage collection inside the timed region (the host loop
+    # only queues work and reads results; a collection pause stalls the queue)
+    gc.collect()
+    gc.disable()
     asr.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
     asr.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     if os.environ.get("ASR_BENCH_REPEAT"):   # diagnostics: the same timed run again, to stderr
         for _ in range(int(os.environ["ASR_BENCH_REPEAT"])):
             asr.synchronize()
