@@ -334,8 +334,8 @@ def main():
     # SIMD) two to a CU, so a batch's decode group is half as many CUs; 1.72 ->
     # 1.89 ms per decode, 5 groups in flight: 64.5 M vs 58.8 M frames/s at 100
     # steps (r2g49), but its first timed run after a short warmup pays ~10 ms
-    # once (20 steps / warmup 5: 27-28 M; r2g50/51, cause not found), so it is
-    # not the default.
+    # once (20 steps / warmup 5: 27-28 M; gone at warmup 20, worse after an
+    # idle 0.1 s: a clock ramp, r2g50/51/58), so it is not the default.
     packed = (args.packed and pipeline and not args.waves and not args.decode_cus and not args.inflight
               and H <= 256 and V + 1 <= 64 and 4 * bcu <= ncu)
     waves = 4 if packed else args.waves
@@ -569,6 +569,8 @@ def main():
     gc.collect()
     gc.disable()
     asr.synchronize()
+    if os.environ.get("ASR_BENCH_SLEEP"):   # diagnostics: idle before the timed region
+        time.sleep(float(os.environ["ASR_BENCH_SLEEP"]))
     t0 = time.perf_counter()
     run(args.steps)
     asr.synchronize()
