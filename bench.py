@@ -9,32 +9,36 @@ already resident in HBM:
 Steps are pipelined by default (--no-pipeline: strictly sequential): the RNN
 and emission projection of batch i+1 run on one HIP stream while batch i is
 decoded on another (event-ordered emission buffers), and up to D batches
-decode at once (--inflight D; auto: D = 3 when the batch needs at most a
-quarter of the CUs at one decode workgroup per utterance and H <= 256, as at
-C2; D = 2 at C5), batch i on decode stream i % D, each stream restricted to
-its own group of CUs and the production stream to the rest
-(hipExtStreamCreateWithCUMask).  One utterance is still decoded by one
-workgroup frame after frame; D only lets the decoder workgroups of several
-batches use CUs one batch leaves idle (C2: 64 workgroups on 256 CUs).  The
-results of batch i come back in one copy of a packed buffer behind its decode
-(an event wait), read on the host once the D-1 younger batches are queued.
-Every step does all of its work inside the timed region.
+decode at once when one batch leaves most CUs idle (--inflight D; auto: D = 3
+when a batch needs at most a quarter of the CUs at one decode workgroup per
+utterance and H <= 256, as at C2; D = 2 at C5), batch i on decode stream
+i % D, each stream restricted to its own group of CUs and the production
+stream to the rest (hipExtStreamCreateWithCUMask).  One utterance is still
+decoded by one workgroup frame after frame.  The results of batch i come back
+in one copy of a packed buffer behind its decode (an event wait), read on the
+host once the D-1 younger batches are queued.  Every step does all of its work
+inside the timed region.
 
-Default workload = BASELINE.json configs[1] (C2): B=64 utterances per GPU,
-T=500 frames, hidden 256, vocab 29, beam 50 (--config C3/C4/C5/BL select the
-other configurations; they are parity-test cases and extra lines, not the
-headline).  Multi-GPU: one process per GPU (torch.distributed.run); rank r
-decodes the contiguous utterance range shard_range(r) with no collective on
-the data path (utterances are independent); weak scaling by
-default (--batch utterances per GPU), strong scaling with --global-batch
-(C4: 2048 utterances split over the GPUs).  After the timed region every
+Default workload = BASELINE.json configs[3] (C4), the configuration the
+metric's 1/2/4/8-GPU line is quoted on: 2048 utterances in all, split over the
+GPUs (strong scaling), T=1000 frames, hidden 256, vocab 29, beam 50 (also
+north_star's >= 10x target shape).  --config C2/C3/C5/BL select the other
+configurations (parity-test cases and extra lines, not the headline).
+
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` with no
+WORLD_SIZE in the environment starts N fresh rank processes itself (this
+parent never touches the GPU and never execs; it exits with the first
+failing rank's status); under torch.distributed.run the ranks come from the
+environment and WORLD_SIZE must equal --gpus.  Rank r decodes the contiguous
+utterance range shard_range(r) with no collective on the data path
+(utterances are independent).  After the timed region every
 rank's hypotheses (labels, fp64 log-prob) are gathered to rank 0 over gloo
 (the host-side gather of north_star), counted against the global batch, and
 checked bit for bit against a 1-GPU decode of the same utterance ids on rank
 0's device.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
-                    [--global-batch G] [--decode-only] [--no-pipeline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
+                    [--global-batch G | --batch B] [--decode-only] [--no-pipeline]
 """
 import argparse
 import ctypes
@@ -192,16 +196,32 @@ def load_profile_json(name: str):
         return None
 
 
-def load_traffic(kernel: str, workload: str):
-    """Measured HBM bytes per launch of `kernel` at `workload` (rocprofv3
-    FETCH_SIZE + WRITE_SIZE passes over this bench at that configuration,
-    summarised by tools/traffic_from_pmc.py into the committed
-    profiles/r02/traffic.json); None when that workload was not profiled."""
-    d = load_profile_json("r02/traffic.json")
+PROFILE_ROUND = "r03"   # profiles/<round>/ holds the counter summaries this line embeds
+
+
+def decoder_variant(V: int, waves: int, max_states: int) -> str:
+    """Template instance of the beam-search kernel a decode ran, as rocprofv3
+    names it without spaces (ctc_beam_v*.hip / ctc_beam_wide.hip tables)."""
+    rpt = 1 if max_states <= 64 else (2 if max_states <= 128 else 4)
+    R = V + 1
+    if R > 64:
+        return f"ctc_wide_kernel<{rpt},false>"
+    cls = 8 if R <= 8 else (32 if R <= 32 else 64)
+    return f"ctc_beam_kernel<{waves},{cls // waves},{rpt},false>"
+
+
+def load_counters(name: str, workload: str, variant: str):
+    """A counter summary (profiles/<round>/<name>.json, written by
+    tools/traffic_from_pmc.py / tools/issue_from_pmc.py from rocprofv3 --pmc
+    passes over this bench) for exactly this workload and kernel variant, with
+    the run it came from; None when that pair was not profiled (a changed
+    kernel or schedule never picks up stale counters)."""
+    d = load_profile_json(f"{PROFILE_ROUND}/{name}.json")
     try:
-        return d[workload][kernel]["hbm_bytes_per_launch"]
+        rec = d[workload][variant]
     except Exception:
         return None
+    return dict(rec, workload=workload, variant=variant)
 
 
 def cpu_share():
@@ -234,12 +254,49 @@ def cpu_model() -> str:
 
 
 # ------------------------------------------------------------------- main
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE and a
+    127.0.0.1 rendezvous in their environment) and wait for them.  The parent
+    makes no GPU call and does not exec: each rank is a fresh child process.
+    Returns 0 when every rank succeeded, else the first failing status (the
+    other ranks are then stopped: they would wait forever at a barrier)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:],
+                                      env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in live:   # the exact children started here, nothing else
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); started by this script when WORLD_SIZE is unset")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="total utterances split over the GPUs (strong scaling)")
@@ -284,6 +341,10 @@ def main():
                          "queues every launch (auto: on when H > 256 and production is not split)")
     ap.add_argument("--result-stream", action="store_true",
                     help="run each batch's traceback on a third stream (measured slower at C2)")
+    ap.add_argument("--dry-run-cpu", action="store_true",
+                    help="no GPU: run the rank launcher, rendezvous, shard plan, gather and "
+                         "1-process check with a host greedy decode standing in for the GPU "
+                         "path (a plumbing rehearsal for CPU tests; prints no throughput)")
     ap.add_argument("--overlap-results", action="store_true",
                     help="queue batch i+1's decode before reading batch i's results "
                          "(measured slower on MI355X: see DESIGN.md §9)")
@@ -298,9 +359,17 @@ def main():
     if args.global_batch is not None:
         cfg["global_batch"] = args.global_batch
 
-    asr = _load("asr_amd", PKG / "asr_amd.py")
-    rank = int(os.environ.get("RANK", "0"))
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"world size {world} (WORLD_SIZE) does not match --gpus {args.gpus}")
+    rank = int(os.environ.get("RANK", "0"))
+    if args.dry_run_cpu:
+        return dry_run_cpu(cfg, rank, world)
+    asr = _load("asr_amd", PKG / "asr_amd.py")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; more ranks than GPUs (a rehearsal on a smaller box)
     # wrap around.  device_count() does not initialise the GPU.
@@ -623,17 +692,25 @@ def main():
     roof = None
     if avg_kernel_ms:
         achieved = bpf * B * T / (avg_kernel_ms * 1e-3) / 1e9
-        kname = "ctc_wide_kernel" if V + 1 > 64 else "ctc_beam_kernel"
-        roof = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 3),
+        ms_, waves_run, _ = decs[last["k"]].config()
+        variant = decoder_variant(V, waves_run, ms_)
+        wl = args.config + (" decode-only" if args.decode_only else "")
+        traffic = load_counters("traffic", wl, variant)
+        issue = load_counters("issue", wl, variant)
+        # The decoder moves ~4V + 8 bytes per live node per frame: the beam
+        # never leaves the CU, so HBM is not what bounds it.  Its limiter is
+        # the per-frame dependency chain on chip (LDS round trips, barriers,
+        # the selection passes), so `bound` names that and `frac` stays the
+        # HBM fraction of SURVEY §8(d)'s algorithmic bytes, for information.
+        roof = {"kernel": variant, "bound": "latency", "achieved": round(achieved, 3),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "frac_of": "HBM roofline (SURVEY §8(d) algorithmic bytes: 4V + 40K per frame)",
                 "avg_launch_ms": round(avg_kernel_ms, 4), "bytes_per_frame": bpf,
                 "frames_per_launch": B * T, "us_per_frame_step": round(1e3 * avg_kernel_ms / T, 4),
-                "traffic": load_traffic(kname, args.config if not args.decode_only else None),
-                "limiter": "on-chip issue/latency (beam resident in LDS; HBM traffic is ~8 MB per "
-                           "launch): see roofline.issue"}
-        iss = load_profile_json("r02/issue.json")
-        if iss and iss.get("workload") == args.config:
-            roof["issue"] = iss.get("issue")
+                "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+                "traffic_source": traffic, "issue": issue,
+                "limiter": "on-chip dependency latency per frame (beam resident in LDS): "
+                           "see roofline.issue for the measured issue/wait fractions"}
 
     mfma = None
     if rank == 0 and world == 1 and not args.decode_only:
@@ -674,6 +751,58 @@ def main():
         d.close()
     asr.synchronize()
     destroy_raw_streams()
+
+
+def greedy_host(T, V, first, count, seed=20261015):
+    """--dry-run-cpu stand-in for a rank's GPU decode: best-path (greedy) CTC
+    over per-utterance random host logits (collapse repeats, drop blank 0).
+    Plumbing only; never a measured or parity-checked path."""
+    lab = np.zeros((count, T), np.int32)
+    ln = np.zeros(count, np.int32)
+    lp = np.zeros(count, np.float64)
+    for b in range(count):
+        e = np.random.default_rng(seed + first + b).standard_normal((T, V))
+        a = e.argmax(1)
+        seq = a[(a != 0) & np.r_[True, a[1:] != a[:-1]]]
+        lab[b, :len(seq)] = seq
+        ln[b] = len(seq)
+        lp[b] = float(e.max(1).sum())
+    return lab, ln, lp
+
+
+def dry_run_cpu(cfg, rank, world):
+    """main()'s multi-rank plumbing with no GPU: gloo rendezvous, the shard
+    plan, each rank's hypotheses gathered to rank 0, merged, counted and
+    checked against one process's result for the whole batch; rank 0 prints
+    one JSON line (n_gpus, gather) without a throughput value."""
+    T, V = cfg["T"], cfg["vocab"]
+    strong = "global_batch" in cfg
+    GB = cfg["global_batch"] if strong else cfg["batch"] * world
+    first, B = shard_range(rank, world, GB) if strong else (shard_first(rank, cfg["batch"]), cfg["batch"])
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    t0 = time.perf_counter()
+    lab, ln, lp = greedy_host(T, V, first, B)
+    elapsed = reduce_max_over_ranks(time.perf_counter() - t0, world)
+    records = gather_hypotheses(pack_hypotheses(first, lab, ln, lp), world, rank)
+    if rank == 0:
+        hyps, lps = merge_records(records)
+        if len(hyps) != GB:
+            raise AssertionError(f"gathered {len(hyps)} hypotheses, expected {GB}")
+        ref = pack_hypotheses(0, *greedy_host(T, V, 0, GB))
+        ok = hyps == ref[1] and np.array_equal(lps, np.asarray(ref[2]))
+        if not ok:
+            raise AssertionError("gathered hypotheses differ from the 1-process result")
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
+                          "dry_run": True, "scaling": "strong" if strong else "weak",
+                          "host_seconds": round(elapsed, 4),
+                          "config": {"global_batch": GB, "T": T, "vocab": V},
+                          "gather": {"utterances": len(hyps), "digest": hyp_digest(hyps, lps)[:16],
+                                     "verified_vs_1process": True}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def cu_masked_streams(mode, B=0):

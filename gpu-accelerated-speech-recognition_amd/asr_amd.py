@@ -40,6 +40,7 @@ ASR_ERR_INTERNAL = 7
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_LOGSOFTMAX = 0, 1, 2, 3
 SEMANTICS_CPU, SEMANTICS_CUDA = 0, 1   # asr_ctc_set_semantics
 ASR_CTC_WAVES_LIST = -1                # asr_ctc_set_waves: the one-wave list kernel
+ASR_CTC_TS_MAX_T = 65536               # longest decode with timesteps on (16-bit frames)
 
 # Every symbol include/asr_amd.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
@@ -492,22 +493,26 @@ class CTCBeamDecoder:
     timesteps [B, beam_width, T] int32, out_lens [B, beam_width] int32);
     hypotheses beyond an utterance's final beam have length 0 and score +inf.
     timesteps[b, k, i] is the frame at which label i of hypothesis k was
-    appended in the surviving search lineage (asr_ctc_set_timesteps; ctcdecode
-    reports the frame of its trie node's best emission, so the two agree in
-    meaning but are not pinned against each other: ctcdecode is unavailable
-    here); -1 past a hypothesis' length.  probs may be a numpy array or a
-    torch tensor (a GPU tensor is decoded in place, no copy)."""
+    FIRST APPENDED in the surviving search lineage (asr_ctc_set_timesteps).
+    This differs from ctcdecode, which reports the frame of its trie node's
+    best emission; the two are not pinned against each other (ctcdecode is
+    unavailable here).  -1 past a hypothesis' length.  Tracking costs a second
+    node table per decode, so it is on only with timesteps=True (the
+    default, as ctcdecode always returns them); timesteps=False returns an
+    all -1 array and decodes on the plain path.  probs may be a numpy array
+    or a torch tensor (a GPU tensor is decoded in place, no copy)."""
 
     def __init__(self, labels: Sequence[str], model_path: Optional[str] = None, alpha: float = 0.0,
                  beta: float = 0.0, cutoff_top_n: int = 40, cutoff_prob: float = 1.0,
                  beam_width: int = 100, num_processes: int = 4, blank_id: int = 0,
-                 log_probs_input: bool = False):
+                 log_probs_input: bool = False, timesteps: bool = True):
         if model_path is not None:
             raise NotImplementedError("language-model scoring is not supported")
         self.labels = list(labels)
         self.beam_width, self.blank_id, self.log_probs_input = beam_width, blank_id, log_probs_input
+        self.track_timesteps = bool(timesteps)
         self._dec = CTCDecoder(len(self.labels), beam_width, blank_id)
-        self._dec.set_timesteps(True)
+        self._dec.set_timesteps(self.track_timesteps)
 
     def decode(self, probs, seq_lens=None):
         B, T, V = (int(x) for x in probs.shape)
@@ -525,7 +530,10 @@ class CTCBeamDecoder:
             arr = probs.cpu().numpy() if hasattr(probs, "cpu") else np.asarray(probs)
             self._dec.decode(arr, is_log=self.log_probs_input, lengths=lens, batch_major=True)
         K = self.beam_width
-        beams = self._dec.beams_ts(max_hyps=self._dec.config()[0])
+        if self.track_timesteps:
+            beams = self._dec.beams_ts(max_hyps=self._dec.config()[0])
+        else:
+            beams = [[(lab, lp, None) for lab, lp in u] for u in self._dec.beams(self._dec.config()[0])]
         results = np.zeros((B, K, T), np.int32)
         scores = np.full((B, K), np.inf, np.float32)
         timesteps = np.full((B, K, T), -1, np.int32)
@@ -534,6 +542,7 @@ class CTCBeamDecoder:
             for k, (lab, lp, ts) in enumerate(hyps[:K]):
                 results[b, k, :len(lab)] = lab
                 scores[b, k] = -lp
-                timesteps[b, k, :len(ts)] = ts
+                if ts is not None:
+                    timesteps[b, k, :len(ts)] = ts
                 out_lens[b, k] = len(lab)
         return results, scores, timesteps, out_lens

@@ -55,6 +55,12 @@ int ctc_launch_decode_v64(const CtcArgs& a, int waves, int rpt, hipStream_t s);
 int ctc_set_max_lds_v8();
 int ctc_set_max_lds_v32();
 int ctc_set_max_lds_v64();
+int ctc_occupancy_v8(const CtcGeom& g, int waves, int rpt);
+int ctc_occupancy_v32(const CtcGeom& g, int waves, int rpt);
+int ctc_occupancy_v64(const CtcGeom& g, int waves, int rpt);
+// Workgroups per CU of the workgroup kernel with `waves` waves (V <= 63, CPU
+// semantics); 0 when that variant is not built or the query fails.
+int ctc_occupancy(const CtcGeom& g, int waves);
 constexpr int WIDE_VMAX = 4096;   // largest vocabulary of the wide kernel (ctc_wide_kernel.inc)
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
 size_t ctc_tile0_bytes(int B, int T);   // a.tile0 workspace of the wide kernel

@@ -58,4 +58,22 @@ int ctc_set_max_lds_v8() {
     return ASR_OK;
 }
 
+// Workgroups of the (waves, rpt) variant that fit on one CU at this layout's
+// LDS size (registers, LDS and wave slots; the runtime's occupancy query), for
+// the automatic schedule choice (runtime.hip auto_waves).  0 if not built.
+int ctc_occupancy_v8(const CtcGeom& g, int waves, int rpt) {
+    const size_t lds = ctc_lds_bytes(g);
+    int n = 0;
+#define X(nw, cw, rp)                                                                        \
+    if (waves == nw && rpt == rp) {                                                          \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                    \
+                &n, ctc_beam_kernel<nw, cw, rp, false>, 64 * nw, lds) != hipSuccess)         \
+            return 0;                                                                        \
+        return n;                                                                            \
+    }
+    ASR_VARIANTS(X)
+#undef X
+    return 0;
+}
+
 }  // namespace asr

@@ -192,6 +192,15 @@ int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s) {
     return ctc_launch_decode_wide(a, rpt, s);
 }
 
+int ctc_occupancy(const CtcGeom& g, int waves) {
+    const int R = g.V + 1;
+    const int rpt = ctc_row_capacity(g.kcap) / 64;
+    if (R <= 8) return ctc_occupancy_v8(g, waves, rpt);
+    if (R <= 32) return ctc_occupancy_v32(g, waves, rpt);
+    if (R <= 64) return ctc_occupancy_v64(g, waves, rpt);
+    return 0;
+}
+
 int ctc_launch_best(const CtcArgs& a, const int* d_codes, int* d_chain, hipStream_t s) {
     hipLaunchKernelGGL(ctc_best_kernel, dim3(a.B), dim3(64), 0, s, a, d_codes, d_chain);
     ASR_LAUNCH_TRY();

@@ -285,6 +285,8 @@ int asr_rnn_bidir_fwd(const float* x, const float* h0, const float* const W_ih[2
 struct asr_ctc {
     int V, beam, blank, K, kcap, waves_override;
     int cu_mode = 0;                // ASR_CTC_SEMANTICS_CUDA
+    int ncu = 0;                    // compute units of the handle's device (auto_waves)
+    int occ8 = -1, occ4 = -1;       // workgroups per CU of the 8- / 4-wave kernels (-1: not queried)
     std::vector<int32_t> codes;
     uint64_t blank_less;
     int device;
@@ -339,12 +341,33 @@ namespace {
 
 asr::CtcGeom plan(const asr_ctc* h, int waves);
 
-// Automatic choice: 8 waves per utterance, measured fastest at C2/C3 and on
-// the bench's emissions.  ASR_CTC_WAVES_LIST (-1) selects the
-// one-wave list kernel (ctc_wave_kernel.inc), faster only on peaked
-// emissions.  valid_waves lowers an explicit count where a narrower
-// instantiation is required.
-int auto_waves(const asr_ctc* h) { (void)h; return 8; }
+// Automatic schedule for a batch of B utterances (one workgroup each).
+// The 8-wave kernel is the fastest per utterance (C2/C3 and the bench's
+// emissions) but, at 153 VGPRs x 2 waves per SIMD, one
+// workgroup fills a CU; the 4-wave kernel (188 VGPRs, one wave per SIMD) fits
+// two per CU.  Measured on MI355X at C2: per-utterance decode
+// time 1.44 ms (8 waves), 1.72 ms (4 waves alone on a CU), 1.89 ms (two
+// 4-wave workgroups sharing a CU).  So once B exceeds the CUs the 8-wave
+// kernel needs ceil(B / ncu) rounds, the 4-wave kernel ceil(B / (2 ncu))
+// rounds of 1.31x the time: 4 waves whenever that is shorter (B > ncu).  The
+// per-CU fit is the runtime's occupancy query of the instantiated kernels
+// (registers, LDS, wave slots), so a layout that does not fit two to a CU
+// keeps 8 waves.  ASR_CTC_WAVES_LIST (-1) selects the one-wave list kernel
+// (ctc_wave_kernel.inc), faster only on peaked emissions.  valid_waves
+// lowers an explicit count where a narrower instantiation is required.
+constexpr double REL_4W_ALONE = 1.72 / 1.44, REL_4W_PAIRED = 1.89 / 1.44;
+int auto_waves(asr_ctc* h, int B) {
+    if (h->cu_mode || h->V + 1 > 64 || h->V + 1 <= 8 || B <= 0) return 8;
+    if (h->occ8 < 0) {   // once per handle: the layout is fixed at creation
+        h->occ8 = asr::ctc_occupancy(plan(h, 8), 8);
+        h->occ4 = asr::ctc_occupancy(plan(h, 4), 4);
+    }
+    if (h->ncu <= 0 || h->occ8 < 1 || h->occ4 < 1) return 8;
+    const long per8 = (long)h->ncu * h->occ8, per4 = (long)h->ncu * h->occ4;
+    const double cost8 = (double)((B + per8 - 1) / per8);
+    const double cost4 = (double)((B + per4 - 1) / per4) * (B > h->ncu ? REL_4W_PAIRED : REL_4W_ALONE);
+    return cost4 < cost8 ? 4 : 8;
+}
 
 // A (waves, vocab class, rows/thread) combination that ctc_beam_v*.hip instantiates.
 int valid_waves(const asr_ctc* h, int waves) {
@@ -478,6 +501,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }
     if (hipGetDevice(&h->device) != hipSuccess ||
+        hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess ||
         hipMalloc(&h->d_codes, sizeof(int) * V) != hipSuccess ||
         hipMemcpy(h->d_codes, h->codes.data(), sizeof(int) * V, hipMemcpyHostToDevice) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
@@ -543,7 +567,10 @@ int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
 
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes) {
     if (!h) return ASR_ERR_ARG;
-    const int w = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h));
+    // the last decode's schedule; before the first decode, that of a batch
+    // with at most one utterance per CU
+    const int w = h->have ? h->last_waves
+                          : valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h, 1));
     if (max_states) *max_states = h->kcap;
     if (waves) *waves = w;
     if (lds_bytes)
@@ -562,6 +589,9 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     if (h_lengths)
         for (int b = 0; b < B; b++)
             if (h_lengths[b] < 0 || h_lengths[b] > T) return ASR_ERR_ARG;
+    // timesteps are stored as 16-bit frame numbers next to the labels (slot
+    // tails, node records, ctc_trace.hip frame_field): frames >= 65536 would wrap
+    if (h->ts && T > ASR_CTC_TS_MAX_T) return ASR_ERR_UNSUPPORTED;
     int rc = ensure_ws(h, B, T);
     if (rc) return rc;
     const hipStream_t st0 = asr_stream(s);
@@ -581,7 +611,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     }
     // .cu-semantics kernels exist for the automatic wave count only; the
     // one-wave list kernel does not track timesteps
-    int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h));
+    int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h, B));
     if (h->ts && waves < 0) waves = valid_waves(h, 8);
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);

@@ -199,7 +199,10 @@ int asr_ctc_get_beams(asr_ctc_t* h, int max_hyps, int max_len, int32_t* h_n_hyps
  * 16 extra bytes per node record and slot.  Off by default; the one-wave
  * list kernel is not used while it is on.  asr_ctc_get_beams_ts returns them
  * as h_timesteps[B][max_hyps][max_len] next to the ranked labels
- * (ASR_ERR_STATE if the decode ran without timesteps). */
+ * (ASR_ERR_STATE if the decode ran without timesteps).  Frames are stored in
+ * 16 bits: with timesteps on, a decode of T > ASR_CTC_TS_MAX_T frames returns
+ * ASR_ERR_UNSUPPORTED (nothing is enqueued). */
+#define ASR_CTC_TS_MAX_T 65536
 int asr_ctc_set_timesteps(asr_ctc_t* h, int on);
 
 /* Stream for the best-path traceback and the copy of its results to host

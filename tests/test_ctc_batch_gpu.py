@@ -84,3 +84,9 @@ def test_ctcdecode_style_mirror_numpy_and_torch_gpu():
     # a GPU tensor is decoded in place (no host copy) and gives the same beams
     res2, scores2, _, lens2 = dec.decode(torch.from_numpy(probs_btv).cuda(), torch.from_numpy(lens))
     assert np.array_equal(res, res2) and np.array_equal(scores, scores2) and np.array_equal(out_lens, lens2)
+    # timesteps=False: the same beams on the plain path, timesteps all -1
+    dec3 = asr.CTCBeamDecoder(["$"] + [chr(65 + i) for i in range(V - 1)], beam_width=beam,
+                              blank_id=0, log_probs_input=True, timesteps=False)
+    res3, scores3, steps3, lens3 = dec3.decode(torch.from_numpy(probs_btv), torch.from_numpy(lens))
+    assert np.array_equal(res, res3) and np.array_equal(scores, scores3) and np.array_equal(out_lens, lens3)
+    assert (steps3 == -1).all()

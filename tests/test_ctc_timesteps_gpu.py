@@ -96,6 +96,18 @@ def test_timesteps_through_overflow_retry():
     assert_ts_equal(got, ref, "uniform")
 
 
+def test_timesteps_frame_limit_guard():
+    """Frames are kept in 16 bits: with timesteps on, T > 65536 is refused
+    before anything is enqueued (no silent wrap of frames >= 65536)."""
+    dec = asr.CTCDecoder(29, 8, 0)
+    dec.set_timesteps(True)
+    buf = asr.DeviceBytes(4 * 29)   # never read: the guard runs first
+    with pytest.raises(asr.AsrError) as ei:
+        dec.decode_device(buf.ptr, asr.ASR_CTC_TS_MAX_T + 1, 1, is_log=True, frame_stride=1, utt_stride=1)
+    assert ei.value.status == asr.ASR_ERR_UNSUPPORTED
+    dec.close()
+
+
 def test_beams_ts_requires_timesteps_mode():
     emis = oracle.synthetic_emissions(10, 2, 29, seed0=1)
     dec = asr.CTCDecoder(29, 8, 0)

@@ -21,7 +21,8 @@ Checked three ways:
     full batch's rows bit for bit (what utterance sharding over GPUs relies
     on);
   * a second kernel schedule (4 waves per utterance instead of 8, V <= 63)
-    must agree bit for bit.
+    must agree bit for bit; the automatic schedule is asserted (8 waves at
+    B <= CUs, the packed 4-wave kernel at C4's one-GPU batch of 2048).
 """
 import hashlib
 import json
@@ -138,6 +139,7 @@ def test_c4_shard_full_size_e2e():
     T, B, H, V, beam = 1000, 256, 256, 29, 50
     em, e = _e2e(T, B, H, V)
     dec, best = decode_best(em.ptr, T, B, V, beam, True)
+    assert dec.config()[1] == 8   # one utterance per CU: the 8-wave kernel
     check_properties(dec, best, V)
     dec.close()
     # oracle on the GPU-produced emissions, 8 full-length utterances
@@ -153,6 +155,33 @@ def test_c4_shard_full_size_e2e():
     d4, best4 = decode_best(em.ptr, T, B, V, beam, True, waves=4)
     d4.close()
     assert best4[0] == best[0] and np.array_equal(best4[1], best[1]), "4-wave schedule differs"
+
+
+def test_c4_one_gpu_full_batch_packed_schedule():
+    """C4 on ONE GPU (the bench's N=1 line): 2048 utterances, more than the
+    CUs, so the library's automatic schedule is the 4-wave kernel two to a CU
+    (runtime.hip auto_waves); it must agree bit for bit with the 8-wave
+    schedule on the whole batch, and its first 256 rows with a 256-utterance
+    decode (one per CU, 8 waves: the 8-GPU shard shape)."""
+    T, B, H, V, beam = 1000, 2048, 256, 29, 50
+    em, e = _e2e(T, B, H, V)
+    dec, best = decode_best(em.ptr, T, B, V, beam, True)
+    assert dec.config()[1] == 4, "automatic schedule for B > CUs should be the packed 4-wave kernel"
+    ms_auto = dec.last_kernel_ms()
+    dec.close()
+    d8, best8 = decode_best(em.ptr, T, B, V, beam, True, waves=8)
+    assert d8.config()[1] == 8
+    ms8 = d8.last_kernel_ms()
+    d8.close()
+    assert best8[0] == best[0] and np.array_equal(best8[1], best[1]), "8-wave schedule differs"
+    ds = asr.CTCDecoder(V, beam, 0)   # rows [0, 256) in place: frame stride B*V
+    ds.decode_device(em.ptr, T, 256, True, frame_stride=B * V, utt_stride=V)
+    l256, p256 = ds.best()
+    assert ds.config()[1] == 8
+    ds.close()
+    assert l256 == best[0][:256] and np.array_equal(p256, best[1][:256]), "256-utterance shard differs"
+    print(f"C4 2048 x 1000 decode: auto (4 waves) {ms_auto:.2f} ms, 8 waves {ms8:.2f} ms")
+    assert ms_auto < ms8, "the automatic schedule should be the faster one at B > CUs"
 
 
 def test_c5_decode_fixture():

@@ -107,3 +107,38 @@ def test_merge_records_rejects_gaps():
     import bench
     with pytest.raises(AssertionError):
         bench.merge_records([(0, [[1]], [0.0]), (2, [[2]], [0.0])])
+
+
+def _run_bench(args, env_extra=None, timeout=300):
+    """bench.py as the driver starts it (`python bench.py --gpus N ...`), in a
+    fresh process without rank variables in its environment."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, env=env, cwd="/tmp",
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("n,extra,gb", [(2, ["--config", "C2", "--T", "40"], 128),    # weak: 64 per rank
+                                        (2, ["--global-batch", "7", "--T", "30"], 7),   # strong, uneven
+                                        (8, ["--T", "60"], 2048)])                      # C4 default, 8 ranks
+def test_bench_self_launches_ranks(n, extra, gb):
+    """`bench.py --gpus N` with no WORLD_SIZE starts N rank processes itself
+    (gloo rendezvous on 127.0.0.1), shards, gathers to rank 0 and checks the
+    gathered batch against one process (--dry-run-cpu: no GPU, a host greedy
+    decode stands in for the GPU path)."""
+    rc, line, err = _run_bench(["--gpus", str(n), "--dry-run-cpu"] + extra)
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == n
+    assert line["gather"]["utterances"] == gb
+    assert line["gather"]["verified_vs_1process"] is True
+
+
+def test_bench_rejects_world_size_mismatch():
+    rc, line, err = _run_bench(["--gpus", "3", "--dry-run-cpu"], env_extra={"WORLD_SIZE": "2"})
+    assert rc != 0 and line is None
+    assert "does not match --gpus 3" in err

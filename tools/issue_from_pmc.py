@@ -1,6 +1,8 @@
 """Summarise a rocprofv3 SQ counter pass over bench.py into
-profiles/r02/issue.json: the decoder kernel's instruction-issue roofline,
-which bench.py embeds as roofline.issue.
+profiles/<round>/issue.json[workload][variant]: the decoder kernel's
+instruction-issue roofline per kernel variant (full template instance),
+which bench.py embeds as roofline.issue when it ran that workload and
+variant.
 
 Counters (one pass, 8 SQ slots): SQ_WAVES, SQ_INSTS_VALU, SQ_INSTS_SALU,
 SQ_INSTS_LDS, SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_WAIT_INST_ANY,
@@ -23,7 +25,7 @@ per CU at the bench's batch, every wave alive for the whole kernel):
                    wave instruction (MI355X_MICROARCH.md §LDS)
 
     python tools/issue_from_pmc.py SQ.csv --kernel ctc_beam_kernel --T 500 --B 64 \
-        --workload C2 [--source label]
+        --workload C2 [--source label] [--round r03]
 """
 import argparse
 import csv
@@ -39,13 +41,18 @@ def main():
     ap.add_argument("--B", type=int, required=True)
     ap.add_argument("--workload", default="C2")
     ap.add_argument("--source", default="")
-    ap.add_argument("--out", default=None)
+    ap.add_argument("--round", default="r03")
     args = ap.parse_args()
     per = {}   # dispatch -> counter -> value
+    variants = set()
     for r in csv.DictReader(open(args.csv)):
         if args.kernel not in r["Kernel_Name"]:
             continue
+        variants.add(r["Kernel_Name"].split("(")[0].replace("void ", "").replace("asr::", "").replace(" ", ""))
         per.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    if len(variants) != 1:
+        raise SystemExit(f"expected one variant of {args.kernel}, found {sorted(variants)}")
+    variant = variants.pop()
     if not per:
         raise SystemExit(f"no {args.kernel} dispatches in {args.csv}")
     keys = sorted({k for d in per.values() for k in d})
@@ -69,12 +76,14 @@ def main():
         "valu_util": round(2.0 * avg["SQ_INSTS_VALU"] / (4 * args.B) / cyc, 4),
         "lds_util": round(2.0 * avg["SQ_INSTS_LDS"] / args.B / cyc, 4),
     }
-    out = {"workload": args.workload, "kernel": args.kernel, "T": args.T, "B": args.B,
+    out = {"T": args.T, "B": args.B,
            "counters_avg_per_launch": {k: round(v) for k, v in avg.items()},
            "issue": issue, "source": args.source}
-    p = Path(args.out) if args.out else Path(__file__).resolve().parents[1] / "profiles" / "r02" / "issue.json"
+    p = Path(__file__).resolve().parents[1] / "profiles" / args.round / "issue.json"
     p.parent.mkdir(parents=True, exist_ok=True)
-    p.write_text(json.dumps(out, indent=1))
+    allw = json.loads(p.read_text()) if p.exists() else {}
+    allw.setdefault(args.workload, {})[variant] = out
+    p.write_text(json.dumps(allw, indent=1))
     print(json.dumps(out, indent=1))
 
 

@@ -1,14 +1,37 @@
 #!/bin/bash
-# rocprofv3 evidence for bench.py (run on the GPU box from the repo root):
-#   1. kernel trace + stats of a short bench run
-#   2. FETCH_SIZE pass, 3. WRITE_SIZE pass (separate: TCC slot limits)
-# Each step under its own time limit; stop on the first failure.
+# rocprofv3 evidence for one bench.py workload (run on the GPU box from the
+# repo root).  Passes, each a separate run under its own time limit (counters
+# never share a run with tracing; one block's slots per pass):
+#   trace  kernel trace + stats
+#   fetch  FETCH_SIZE            write  WRITE_SIZE
+#   sq     8 SQ issue counters   grbm   GRBM_GUI_ACTIVE GRBM_COUNT
+# Stops at the first failing pass.  Summaries are made on the dev side:
+#   tools/traffic_from_pmc.py, tools/issue_from_pmc.py -> profiles/<round>/
+#
+#   OUT=c4 BENCH_ARGS="--steps 5 --warmup 2 --no-cpu-baseline" PASSES="trace fetch write sq" \
+#       bash tools/profile_bench.sh
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/rocprof
-mkdir -p $OUT
+OUT=gpurun_out/prof_${OUT:-run}
+mkdir -p "$OUT"
 ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace failed $?"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 || { echo "fetch pass failed $?"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1 || { echo "write pass failed $?"; exit 1; }
-find $OUT -name "*.csv" | head -50
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+for pass in ${PASSES:-trace fetch write}; do
+    case $pass in
+        trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1 ;;
+        fetch) timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 ;;
+        write) timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 ;;
+        sq)    timeout -s KILL 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/sq" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/sq.log" 2>&1 ;;
+        grbm)  timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/grbm" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/grbm.log" 2>&1 ;;
+        *) echo "unknown pass $pass"; exit 2 ;;
+    esac
+    rc=$?
+    echo "pass $pass rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+done
+find "$OUT" -name "*.csv"

@@ -1,7 +1,8 @@
 """Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into
-profiles/r02/traffic.json (HBM bytes per launch of each kernel, keyed by the
-bench workload the passes ran), which bench.py embeds as roofline.traffic for
-that workload only.
+profiles/<round>/traffic.json: HBM bytes per launch of each kernel variant
+(the full template instance, e.g. ctc_beam_kernel<4,8,1,false>), keyed by the
+bench workload the passes ran.  bench.py embeds the entry of the workload and
+decoder variant it actually ran as roofline.traffic, with its source label.
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md:
 FETCH_SIZE reads exactly half the bytes of 16-B/lane coalesced streaming
@@ -9,7 +10,7 @@ reads; the decoder's emission loads are 4-B/lane global_load_dword, for
 which the counter is not halved (checked: 4055 KiB vs 3.71 MB of emission
 rows per C2 launch), so no correction is applied to the decoder.
 
-    python tools/traffic_from_pmc.py FETCH.csv WRITE.csv WORKLOAD [source-label]
+    python tools/traffic_from_pmc.py FETCH.csv WRITE.csv WORKLOAD [source-label] [round]
 """
 import csv
 import json
@@ -21,8 +22,7 @@ def per_kernel(path):
     agg = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        short = name.split("(")[0].replace("void ", "").replace("asr::", "")
-        short = short.split("<")[0]
+        short = name.split("(")[0].replace("void ", "").replace("asr::", "").replace(" ", "")
         agg.setdefault(short, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
@@ -31,7 +31,9 @@ def main():
     fetch, write = per_kernel(sys.argv[1]), per_kernel(sys.argv[2])
     workload = sys.argv[3]
     label = sys.argv[4] if len(sys.argv) > 4 else ""
-    p = Path(__file__).resolve().parents[1] / "profiles" / "r02" / "traffic.json"
+    rnd = sys.argv[5] if len(sys.argv) > 5 else "r03"
+    p = Path(__file__).resolve().parents[1] / "profiles" / rnd / "traffic.json"
+    p.parent.mkdir(parents=True, exist_ok=True)
     allw = json.loads(p.read_text()) if p.exists() else {}
     out = {}
     for k in sorted(set(fetch) & set(write)):
