@@ -736,7 +736,8 @@ def main():
                        f": B={B}/GPU (global {GB}), T={T}, hidden={H}, vocab={V}, beam={beam}",
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
-                       "inflight_decodes": D, "production_streams": Pn, "decode_waves": waves or 8,
+                       "inflight_decodes": D, "production_streams": Pn,
+                       "decode_waves": decs[last["k"]].config()[1],   # the schedule the decodes ran
                        "decode_cus_per_batch": gcu if pipeline and D > 1 else None,
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
                                     "on another" + split_note +

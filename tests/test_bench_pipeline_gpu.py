@@ -16,9 +16,9 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _bench(*args):
+def _bench(*args, config="C2"):
     cmd = [sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", "--steps", "6", "--warmup", "2",
-           "--T", "100", *args]
+           "--T", "100", "--config", config, *args]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
@@ -40,3 +40,17 @@ def test_inflight_and_split_production_match_sequential():
     assert runs["d3_split_all"]["config"]["inflight_decodes"] == 3
     assert runs["packed"]["config"]["decode_waves"] == 4 and runs["packed"]["config"]["inflight_decodes"] == 5
     assert runs["d2_unsplit_graph"]["config"]["production_streams"] == 2
+
+
+def test_c4_self_launched_ranks_match_one_rank():
+    """The driver's multi-GPU form, `bench.py --gpus 2` with no rank
+    variables: two rank processes (sharing this box's one GPU: ranks wrap)
+    shard C4's 2048 utterances; rank 0 gathers and re-decodes every shard on
+    its own device (verified_vs_1gpu), and the digest equals one rank's."""
+    one = _bench(config="C4")
+    two = _bench("--gpus", "2", config="C4")
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert one["gather"]["utterances"] == two["gather"]["utterances"] == 2048
+    assert two["gather"]["verified_vs_1gpu"] is True
+    assert two["gather"]["digest"] == one["gather"]["digest"]
+    assert two["scaling"] == "strong" and two["config"]["batch_per_gpu"] == 1024
