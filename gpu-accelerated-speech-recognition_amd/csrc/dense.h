@@ -29,6 +29,9 @@ struct GemmArgs {
 int gemm_launch(const GemmArgs& g, int epi, hipStream_t s);
 int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                      float* hid, int T, int B, int H, hipStream_t s);
+// The same recurrence on MFMA, 16 utterances per workgroup (H <= 256, H % 16 == 0).
+int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
+                          float* hid, int T, int B, int H, hipStream_t s);
 int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
 int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
 int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);

@@ -438,6 +438,148 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 }
 
 // ---------------------------------------------------------------------------
+// RNN recurrence on MFMA for large batches, H <= 256, H % 16 == 0:
+// h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)), in place over P (as
+// rnn_recur_kernel).  The VALU kernel above runs one utterance per CU, so
+// its step is a GEMV whose 65k FMAs take ~2,200 cycles of dependent latency;
+// at B >> CUs that is ~36 k CU-cycles per 16 utterance-steps.  Here a
+// workgroup carries 16 utterances: one step is a [16 x H] . [H x H] GEMM on
+// v_mfma_f32_16x16x4f32 (exact fp32), ~8 k cycles per 16 utterance-steps at
+// H = 256 — compute-bound at the MFMA rate (64 FLOP/clk/SIMD).
+//   * ceil(H/32) waves; wave w owns the 16-column tiles 2w and 2w + 1 and
+//     keeps their W_hh columns in registers for the whole sequence (H/2
+//     floats per lane: 128 VGPRs at H = 256, two waves per SIMD), loaded once.
+//   * h_{t-1} (16 x H) lives in LDS, double-buffered: one barrier per step.
+//     MFMA (i, e) of lane group g = lane >> 4 contracts k = 16i + 4g + e for
+//     both operands (a bijection of the H k-slots), so each lane reads its A
+//     fragments with one ds_read_b128 per 16 k, shared by its two tiles.
+//   * Two accumulator chains per tile (even / odd 16-k chunks), summed at
+//     the end: dependent MFMA latency (40 cycles) never stalls the issue.
+//   * Epilogue per lane and tile: rows 4g + j (j < 4), column
+//     16 tile + (lane & 15): P_t (prefetched one step ahead) + h.W_hh,
+//     + bias, tanh (op order of RNN_Cell.cu:10-12); to LDS for the next
+//     step and to hid.
+// Grid ceil(B / 16); block 64 * ceil(H / 32) threads.
+// ---------------------------------------------------------------------------
+constexpr int RM_ROWS = 16;
+constexpr int RM_LD = RNN_HMAX + 4;   // LDS row stride (floats): b128 reads of a quarter-wave hit distinct banks
+constexpr int RM_NCH = RNN_HMAX / 16;  // 16-k chunks at H = 256
+
+__global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __restrict__ h0,
+                                                             const float* __restrict__ Whh,
+                                                             const float* __restrict__ b_ih,
+                                                             const float* __restrict__ b_hh,
+                                                             float* __restrict__ hid, int T, int B,
+                                                             int H) {
+    __shared__ __attribute__((aligned(16))) float hs[2][RM_ROWS * RM_LD];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    const int nch = H >> 4;                 // 16-k chunks = 16-column tiles
+    const int r0 = blockIdx.x * RM_ROWS;
+    const int nthr = (int)blockDim.x;
+    bool tv[2];                             // tile 2w + tt exists
+    int n[2];                               // this lane's column in tile 2w + tt
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++) {
+        tv[tt] = 2 * w + tt < nch;
+        n[tt] = tv[tt] ? (2 * w + tt) * 16 + c : 0;
+    }
+    // W_hh columns: wb[tt][i][e] = W_hh[16i + 4g + e][n[tt]]
+    float wb[2][RM_NCH][4];
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+        for (int i = 0; i < RM_NCH; i++)
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                wb[tt][i][e] = (tv[tt] && i < nch) ? Whh[(long)(16 * i + 4 * g + e) * H + n[tt]] : 0.f;
+    // h_{-1}: rows of h0 (zeros when NULL, RNN.h:15-16) into buffer 0
+    for (int x = tid; x < RM_ROWS * H; x += nthr) {
+        const int r = x / H, k = x - r * H;
+        hs[0][r * RM_LD + k] = (h0 && r0 + r < B) ? h0[(long)(r0 + r) * H + k] : 0.f;
+    }
+    float bias[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++) bias[tt] = tv[tt] ? b_hh[n[tt]] + b_ih[n[tt]] : 0.f;
+    const long tstride = (long)B * H;
+    int rowoff[4];   // B * H < 2^31 (checked at launch)
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int r = r0 + 4 * g + j;
+        ok[j] = r < B;
+        rowoff[j] = (ok[j] ? r : 0) * H;
+    }
+    float pn[2][4];
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) pn[tt][j] = (tv[tt] && ok[j]) ? hid[rowoff[j] + n[tt]] : 0.f;
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < T; t++) {
+        float p[2][4];
+#pragma unroll
+        for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) p[tt][j] = pn[tt][j];
+        float* base = hid + (long)t * tstride;
+        if (t + 1 < T) {
+#pragma unroll
+            for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    pn[tt][j] = (tv[tt] && ok[j]) ? base[tstride + rowoff[j] + n[tt]] : 0.f;
+        }
+        const float* hrow = &hs[cur][c * RM_LD + 4 * g];
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+            for (int u = 0; u < 2; u++) acc[tt][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < RM_NCH; i++) {
+            if (i < nch) {
+                const float4 a = *reinterpret_cast<const float4*>(hrow + 16 * i);
+#pragma unroll
+                for (int tt = 0; tt < 2; tt++) {
+                    f32x4& q = acc[tt][i & 1];
+                    q = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[tt][i][0], q, 0, 0, 0);
+                    q = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[tt][i][1], q, 0, 0, 0);
+                    q = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wb[tt][i][2], q, 0, 0, 0);
+                    q = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wb[tt][i][3], q, 0, 0, 0);
+                }
+            }
+        }
+        float* hn = hs[cur ^ 1];
+#pragma unroll
+        for (int tt = 0; tt < 2; tt++) {
+            const f32x4 sum = acc[tt][0] + acc[tt][1];
+            if (!tv[tt]) continue;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float h = tanhf((p[tt][j] + sum[j]) + bias[tt]);
+                hn[(4 * g + j) * RM_LD + n[tt]] = h;
+                if (ok[j]) base[rowoff[j] + n[tt]] = h;
+            }
+        }
+        cur ^= 1;
+        lds_barrier();
+    }
+}
+
+int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
+                          float* hid, int T, int B, int H, hipStream_t s) {
+    if (H > RNN_HMAX || (H & 15) != 0 || B <= 0) return ASR_ERR_UNSUPPORTED;
+    if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
+    hipLaunchKernelGGL(rnn_recur_mfma_kernel, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
+                       dim3(64 * ((H / 16 + 1) / 2)), 0, s,
+                       h0, Whh, b_ih, b_hh, hid, T, B, H);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // One recurrence step for H > 256 (W_hh too large to stay on one CU):
 // h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)) in place over P_t
 // (RNN_Cell.cu:10-12 order).  Small M (the batch) and wide N: each

@@ -174,12 +174,32 @@ int asr_rnn_cell_fwd(const float* x, const float* h_prev, const float* W_ih, con
     g.b1 = b_ih; g.b2 = b_hh;
     return asr::gemm_launch(g, asr::EPI_DUAL_TANH, asr_stream(s));
 }
+// H <= 256: the VALU kernel (one utterance per CU, W_hh in registers) has
+// the shortest step, ~0.9 us, but costs a whole CU per utterance; the MFMA
+// kernel carries 16 utterances per CU at ~3.4 us per step (H = 256).  With
+// B utterances on n CUs the VALU kernel needs ceil(B / n) rounds, the MFMA
+// kernel ceil(B / 16n) rounds of ~3.7x the step: MFMA from B >= 4n on (and
+// it leaves CUs free for concurrent work well before that).
+// ASR_RNN_MFMA=0/1 forces the choice (A/B timing).
+static bool rnn_use_mfma(int B, int H) {
+    if ((H & 15) != 0) return false;
+    if (const char* f = getenv("ASR_RNN_MFMA")) return atoi(f) != 0;
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        return false;
+    return B >= 4 * ncu;
+}
+
 // Recurrence over a hid buffer that already holds the input projection
 // P_t = x_t . W_ih, in place: hid[t] = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)).
 static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
                           const float* b_hh, float* hid, int T, int B, int H, hipStream_t st) {
     int rc = ASR_OK;
-    if (H <= 256) return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+    if (H <= 256) {
+        if (rnn_use_mfma(B, H)) return asr::rnn_recur_mfma_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+        return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+    }
     // H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
     // h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
     // H % 128 == 0, else the VALU kernel with W_hh slices in LDS.

@@ -177,6 +177,62 @@ def test_rnn_recur_stage_equals_rnn_fwd(T, B, I, H):
         asr.rnn_recur_fwd(w_hh, b_ih, b_hh, hid, 0, B)
 
 
+@pytest.mark.parametrize("T,B,I,H", [(30, 37, 64, 256), (9, 16, 24, 48), (7, 5, 16, 16), (12, 50, 40, 128),
+                                     (6, 33, 8, 80)])
+def test_rnn_forward_mfma_recurrence(T, B, I, H, monkeypatch):
+    """H <= 256, H % 16 == 0: the MFMA recurrence (16 utterances per
+    workgroup, W_hh in registers; ragged last tile, odd tile counts), forced
+    with ASR_RNN_MFMA=1, against torch.nn.RNN in fp32, with and without h0;
+    the recurrence stage alone (asr_rnn_recur_fwd) gives the same bits."""
+    monkeypatch.setenv("ASR_RNN_MFMA", "1")
+    rng = np.random.default_rng(T * 7 + H)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    W = [dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1))]
+    hid = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dm(x), *W, hid, T, B)
+    close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 5e-5)
+    asr.rnn_fwd(dm(x), *W, hid, T, B, h0=dm(h0))
+    got = hid.toCpu()
+    close(got, _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 5e-5)
+    hid2 = asr.DeviceMatrix(T * B, H)
+    asr.linear_fwd(dm(x), W[0], None, hid2, asr.EPI_NONE)
+    asr.rnn_recur_fwd(W[1], W[2], W[3], hid2, T, B, h0=dm(h0))
+    assert np.array_equal(hid2.toCpu(), got)
+
+
+def test_rnn_recurrence_schedule_choice(monkeypatch):
+    """Without the override the library picks the MFMA recurrence at
+    B >= 4 x CUs (C4's one-GPU batch of 2048) and the VALU one below it; both
+    agree with torch.  C4's shapes, T shortened."""
+    monkeypatch.delenv("ASR_RNN_MFMA", raising=False)
+    T, I, H = 8, 256, 256
+    rng = np.random.default_rng(4)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    W = [dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1))]
+    for B in (256, 2048):
+        x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+        hid = asr.DeviceMatrix(T * B, H)
+        asr.rnn_fwd(dm(x), *W, hid, T, B)
+        close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 5e-5)
+        # the forced other schedule agrees to fp32 rounding (different sum order)
+        monkeypatch.setenv("ASR_RNN_MFMA", "0" if B == 2048 else "1")
+        hid2 = asr.DeviceMatrix(T * B, H)
+        asr.rnn_fwd(dm(x), *W, hid2, T, B)
+        monkeypatch.delenv("ASR_RNN_MFMA")
+        close(hid2.toCpu(), hid.toCpu(), 5e-5)
+        assert not np.array_equal(hid2.toCpu(), hid.toCpu()), "expected two distinct kernels"
+
+
 def test_rnn_cell_forward():
     rng = np.random.default_rng(5)
     B, I, H = 17, 33, 70
