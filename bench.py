@@ -410,15 +410,25 @@ def main():
     waves = 4 if packed else args.waves
     gcu = min(ncu, args.decode_cus or (-(-B // 16) * 8 if packed else bcu))
     D = 1
+    plain = False   # D decodes share every CU (no CU masks): batches that fill the chip
     if pipeline:
         # auto: up to 3 decode groups for H <= 256 (C2: 38.7 M vs 21.1 M frames/s at
         # D = 1), 2 for the H = 1024 recurrence (C5: D = 2 3.48 M, D = 3 2.99 M,
         # gpurun_out/r2g31); packed: 5 (one recurrence group of bcu CUs beside them)
         if packed:
             D = max(1, min(5, (ncu - bcu) // gcu))
+        elif 2 * bcu > ncu and H <= 256 and V + 1 <= 64 and not args.decode_cus:
+            # A batch fills the chip (C4's shards: 256 utterances per GPU at 8
+            # GPUs).  Consecutive batches then decode concurrently on plain
+            # streams until ~3 utterances share each CU — the library packs
+            # them three 4-wave workgroups to a CU (asr_ctc_set_concurrency);
+            # C4 on one GPU (2048 = 8 per CU) needs no second batch.
+            u = -(-B // ncu)
+            D = args.inflight or max(1, -(-3 // u))
+            plain = D > 1
         else:
             D = args.inflight or max(1, min(3 if H <= 256 else 2, ncu // gcu - 1))
-        if D > 1 and (D + 1) * gcu > ncu:
+        if D > 1 and not plain and (D + 1) * gcu > ncu:
             raise SystemExit(f"--inflight {D}: {D} decode groups of {gcu} CUs + production exceed {ncu} CUs")
     # Buffer i % nbuf holds batch i.  D batches are decoding while batch i+1 is
     # produced, and a buffer is only produced into after its batch's results
@@ -434,21 +444,31 @@ def main():
     d_hid = [asr.DeviceMatrix(T * B, H) for _ in range(nbuf)]
     d_emis = [asr.DeviceMatrix(T * B, V) for _ in range(nbuf)]
     decs = [asr.CTCDecoder(V, beam, 0, waves=waves) for _ in range(nbuf)]
+    if plain:   # D decodes of B utterances share the CUs: schedule for D x B
+        for d in decs:
+            d.set_concurrency(D)
     if pipeline:   # HIP streams/events via torch (same HIP runtime as libasr_amd)
         torch.cuda.set_device(local)
         s_prod, s_dec = torch.cuda.Stream(), torch.cuda.Stream()
         s_decs = [s_dec]
         split = args.cu_split
-        if D > 1:
+        if plain:
+            split = "plain"
+            s_decs = [torch.cuda.Stream() for _ in range(D)]
+            s_dec = s_decs[0]
+        elif D > 1:
             split = "groups"
             s_prod, s_decs = cu_group_streams(D, gcu, ncu)
             s_dec = s_decs[0]
         elif split == "auto":   # one decode workgroup per utterance, one per CU
             split = "half" if B <= ncu // 2 else "none"   # fit: equal at C2, slower at C5 (r2g28)
-        if split not in ("none", "groups"):   # the RNN's workgroups then never share a CU with the decoder's
+        if split not in ("none", "groups", "plain"):   # the RNN's workgroups then never share a CU with the decoder's
             s_prod, s_dec = cu_masked_streams(split, B)
             s_decs = [s_dec]
-        split_note = {"none": "", "half": "; decode on CUs [0, n/2), production on [n/2, n)",
+        split_note = {"none": "", "plain": f"; {D} batches decoding at once on plain streams (batch i on stream "
+                                           f"i % {D}), every CU shared, decoders scheduled for {D} x {B} "
+                                           f"utterances (asr_ctc_set_concurrency)",
+                      "half": "; decode on CUs [0, n/2), production on [n/2, n)",
                       "fit": f"; decode on CUs [0, {gcu}) (one per utterance), production on the rest",
                       "interleave": "; decode on even CUs, production on odd",
                       "groups": f"; {D} batches decoding at once, batch i on stream i % {D} restricted to "
@@ -738,7 +758,7 @@ def main():
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
                        "inflight_decodes": D, "production_streams": Pn,
                        "decode_waves": decs[last["k"]].config()[1],   # the schedule the decodes ran
-                       "decode_cus_per_batch": gcu if pipeline and D > 1 else None,
+                       "decode_cus_per_batch": gcu if pipeline and D > 1 and not plain else None,
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
                                     "on another" + split_note +
                                     ("; tracebacks on a third stream" if args.result_stream else "")

@@ -54,6 +54,7 @@ EXPORTS = [
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
+    "asr_ctc_set_concurrency",
 ]
 
 
@@ -114,6 +115,7 @@ def lib() -> ctypes.CDLL:
         "asr_ctc_get_beams": [_vp, _i, _i, _vp, _vp, _vp, _vp],
         "asr_ctc_last_kernel_ms": [_vp, ctypes.POINTER(_f)],
         "asr_ctc_set_waves": [_vp, _i],
+        "asr_ctc_set_concurrency": [_vp, _i],
         "asr_ctc_get_config": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_ctc_decode_ex": [_vp, _vp, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
         "asr_ctc_set_semantics": [_vp, _i],
@@ -346,6 +348,11 @@ class CTCDecoder:
 
     def set_waves(self, waves: int) -> None:
         check(lib().asr_ctc_set_waves(self.h, waves), "asr_ctc_set_waves")
+
+    def set_concurrency(self, n: int) -> None:
+        """Scheduling hint: n decodes of this batch size run at once on the
+        device (asr_ctc_set_concurrency); results are unchanged."""
+        check(lib().asr_ctc_set_concurrency(self.h, int(n)), "asr_ctc_set_concurrency")
 
     def set_semantics(self, semantics: int) -> None:
         """SEMANTICS_CPU (default, the parity target) or SEMANTICS_CUDA

@@ -307,6 +307,7 @@ struct asr_ctc {
     int cu_mode = 0;                // ASR_CTC_SEMANTICS_CUDA
     int ncu = 0;                    // compute units of the handle's device (auto_waves)
     int occ8 = -1, occ4 = -1;       // workgroups per CU of the 8- / 4-wave kernels (-1: not queried)
+    int concurrency = 1;            // decodes of this size in flight on the device (asr_ctc_set_concurrency)
     std::vector<int32_t> codes;
     uint64_t blank_less;
     int device;
@@ -362,20 +363,22 @@ namespace {
 asr::CtcGeom plan(const asr_ctc* h, int waves);
 
 // Automatic schedule for a batch of B utterances (one workgroup each).
-// The 8-wave kernel is the fastest per utterance (C2/C3 and the bench's
-// emissions) but, at 153 VGPRs x 2 waves per SIMD, one
-// workgroup fills a CU; the 4-wave kernel (188 VGPRs, one wave per SIMD) fits
-// two per CU.  Measured on MI355X at C2: per-utterance decode
-// time 1.44 ms (8 waves), 1.72 ms (4 waves alone on a CU), 1.89 ms (two
-// 4-wave workgroups sharing a CU).  So once B exceeds the CUs the 8-wave
-// kernel needs ceil(B / ncu) rounds, the 4-wave kernel ceil(B / (2 ncu))
-// rounds of 1.31x the time: 4 waves whenever that is shorter (B > ncu).  The
-// per-CU fit is the runtime's occupancy query of the instantiated kernels
-// (registers, LDS, wave slots), so a layout that does not fit two to a CU
-// keeps 8 waves.  ASR_CTC_WAVES_LIST (-1) selects the one-wave list kernel
+// The 8-wave kernel is the fastest per utterance but, at 153
+// VGPRs x 2 waves per SIMD, one workgroup fills a CU; the 4-wave kernel fits
+// three per CU (167 VGPRs, ctc_waves_per_eu).  Measured on MI355X, C4 shapes
+// on the bench's emissions (tools/occupancy_sweep.py, profiles/r03/): per-
+// utterance frame time relative to the 8-wave kernel alone on a CU is 1.13
+// (4 waves alone), 1.25 (two 4-wave workgroups sharing a CU), 1.46 (three).
+// With u = ceil(B / ncu) utterances per CU the 8-wave kernel runs u rounds;
+// the 4-wave kernel floor(u / n) rounds of n per CU plus one of the rest:
+// 4 waves whenever that is shorter, i.e. from B > ncu on.  The per-CU fit n
+// is the runtime's occupancy query of the instantiated kernels (registers,
+// LDS, wave slots), so a layout that does not fit several to a CU keeps 8
+// waves.  ASR_CTC_WAVES_LIST (-1) selects the one-wave list kernel
 // (ctc_wave_kernel.inc), faster only on peaked emissions.  valid_waves
 // lowers an explicit count where a narrower instantiation is required.
-constexpr double REL_4W_ALONE = 1.72 / 1.44, REL_4W_PAIRED = 1.89 / 1.44;
+constexpr double REL_4W[4] = {0.0, 1.13, 1.25, 1.46};
+double rel_4w(int n) { return n <= 3 ? REL_4W[n] : REL_4W[3] * n / 3.0; }
 int auto_waves(asr_ctc* h, int B) {
     if (h->cu_mode || h->V + 1 > 64 || h->V + 1 <= 8 || B <= 0) return 8;
     if (h->occ8 < 0) {   // once per handle: the layout is fixed at creation
@@ -383,9 +386,10 @@ int auto_waves(asr_ctc* h, int B) {
         h->occ4 = asr::ctc_occupancy(plan(h, 4), 4);
     }
     if (h->ncu <= 0 || h->occ8 < 1 || h->occ4 < 1) return 8;
-    const long per8 = (long)h->ncu * h->occ8, per4 = (long)h->ncu * h->occ4;
-    const double cost8 = (double)((B + per8 - 1) / per8);
-    const double cost4 = (double)((B + per4 - 1) / per4) * (B > h->ncu ? REL_4W_PAIRED : REL_4W_ALONE);
+    const int u = (B + h->ncu - 1) / h->ncu;   // utterances on the busiest CU
+    const double cost8 = (double)((u + h->occ8 - 1) / h->occ8);
+    const int n4 = h->occ4;
+    const double cost4 = (u / n4) * rel_4w(n4) + (u % n4 ? rel_4w(u % n4) : 0.0);
     return cost4 < cost8 ? 4 : 8;
 }
 
@@ -577,6 +581,12 @@ int asr_ctc_set_timesteps(asr_ctc_t* h, int on) {
     return ASR_OK;
 }
 
+int asr_ctc_set_concurrency(asr_ctc_t* h, int n) {
+    if (!h || n < 1) return ASR_ERR_ARG;
+    h->concurrency = n;
+    return ASR_OK;
+}
+
 int asr_ctc_set_waves(asr_ctc_t* h, int waves) {
     if (!h || !(waves == ASR_CTC_WAVES_LIST || waves == 0 || waves == 1 || waves == 2 || waves == 4 ||
                 waves == 8))
@@ -631,7 +641,8 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     }
     // .cu-semantics kernels exist for the automatic wave count only; the
     // one-wave list kernel does not track timesteps
-    int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h, B));
+    const long Beff = std::min<long>((long)B * h->concurrency, 1L << 30);
+    int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h, (int)Beff));
     if (h->ts && waves < 0) waves = valid_waves(h, 8);
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);

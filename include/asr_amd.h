@@ -236,6 +236,12 @@ int asr_ctc_set_semantics(asr_ctc_t* h, int semantics);
  * get_config reports the schedule a decode will use (ASR_CTC_WAVES_LIST or 1..8). */
 #define ASR_CTC_WAVES_LIST (-1)
 int asr_ctc_set_waves(asr_ctc_t* h, int waves);
+/* Scheduling hint: n decodes of this handle's batch size are in flight on
+ * the device at once (e.g. a caller pipelining n batches on n streams;
+ * default 1).  The automatic schedule is then chosen for n x B utterances
+ * sharing the CUs — from two per CU on, the 4-wave kernel several
+ * workgroups to a CU.  Never changes results. */
+int asr_ctc_set_concurrency(asr_ctc_t* h, int n);
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes);
 
 #ifdef __cplusplus
