@@ -271,6 +271,137 @@ static int launch_gemm_narrow(const GemmArgs& g, hipStream_t s) {
     return ASR_OK;
 }
 
+// Tall-skinny wide GEMMs (the RNN input projection, [T*B, in] x [in, H] with
+// in <= 512, H >= 128: C4 is 2.05 M x 256 x 256 per GPU): the tiled kernel
+// re-stages B through LDS for every 64-row tile and barriers twice per
+// 16-deep K stage (81 TFLOP/s, 52 % of the fp32 MFMA peak).  Here a
+// persistent workgroup keeps a BNW-column slice of B^T in LDS for its whole
+// life (K x BNW floats, loaded once) and streams 128-row tiles of A straight
+// into registers — the narrow kernel's A path: lane (r, g) holds row r's
+// float4 at k = 16i + 4g, so MFMA (i, e) contracts k = 16i + 4g + e and its B
+// fragment is one ds_read_b128 of B^T — with the next tile's A in flight
+// during this tile's MFMAs.  No barrier after the B staging.  One workgroup
+// per CU (the slice takes most of the LDS); grid = column slices x row groups.
+constexpr int GW_W = 8;     // waves per workgroup: 8 x 16 = 128 rows per tile
+template <int BNW, int KMAX, int EPI>
+__global__ __launch_bounds__(64 * GW_W) void gemm_wide_kernel(GemmArgs g) {
+    constexpr int NT = BNW / 16;
+    constexpr int NI = KMAX / 16;
+    constexpr int BTS = KMAX + 4;   // B^T row stride (floats)
+    extern __shared__ __attribute__((aligned(16))) float smem_gw[];
+    float* Bt = smem_gw;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, gq = lane >> 4;
+    const int n0 = blockIdx.y * BNW;
+    const int K = g.K;
+    for (int idx = tid; idx < K * BNW; idx += 64 * GW_W) {   // B^T slice, zero past N
+        const int k = idx / BNW, n = idx - k * BNW;
+        Bt[n * BTS + k] = n0 + n < g.N ? g.B[(long)k * g.sbk + n0 + n] : 0.f;
+    }
+    const int ntile = (g.M + 16 * GW_W - 1) / (16 * GW_W);
+    int tile = blockIdx.x;
+    f32x4 a[NI];
+    auto load_a = [&](int tl) {
+        const int row = tl * (16 * GW_W) + w * 16 + r;
+        const bool rok = tl < ntile && row < g.M;
+        const float* arow = g.A + (long)(rok ? row : 0) * g.sam;
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const int k = 16 * i + 4 * gq;
+            a[i] = (rok && k < K) ? *reinterpret_cast<const f32x4*>(arow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    load_a(tile);
+    __syncthreads();
+    for (; tile < ntile; tile += gridDim.x) {
+        f32x4 acc[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // each K quarter's registers are refilled with the next tile's A as
+        // soon as its MFMAs have consumed them, so the loads of the next tile
+        // are in flight during the rest of this one (64 A VGPRs in all)
+        const int nrow = (tile + (int)gridDim.x) * (16 * GW_W) + w * 16 + r;
+        const bool nok = tile + (int)gridDim.x < ntile && nrow < g.M;
+        const float* nrowp = g.A + (long)(nok ? nrow : 0) * g.sam;
+        // B fragments one k-chunk ahead (NT b128 reads), fenced so that the
+        // scheduler does not hoist all NI x NT reads at once (512 VGPRs)
+        const float* btp = &Bt[r * BTS + 4 * gq];
+        f32x4 bc[NT], bn[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) bc[nt] = *reinterpret_cast<const f32x4*>(btp + nt * 16 * BTS);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+#pragma unroll
+            for (int ii = 0; ii < NI / 4; ii++) {
+                const int i = q * (NI / 4) + ii;
+                if (i + 1 < NI) {
+#pragma unroll
+                    for (int nt = 0; nt < NT; nt++)
+                        bn[nt] = *reinterpret_cast<const f32x4*>(btp + nt * 16 * BTS + 16 * (i + 1));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int nt = 0; nt < NT; nt++) {
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], bc[nt][e], acc[nt], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int nt = 0; nt < NT; nt++) bc[nt] = bn[nt];
+            }
+#pragma unroll
+            for (int ii = 0; ii < NI / 4; ii++) {
+                const int i = q * (NI / 4) + ii;
+                const int k = 16 * i + 4 * gq;
+                a[i] = (nok && k < K) ? *reinterpret_cast<const f32x4*>(nrowp + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        gemm_epilogue<BNW, EPI>(g, acc, acc, tile * (16 * GW_W) + w * 16 + gq * 4, n0, lane);
+    }
+}
+
+template <int BNW, int KMAX, int EPI>
+static int launch_gemm_wide_k(const GemmArgs& g, hipStream_t s) {
+    const size_t lds = sizeof(float) * (size_t)BNW * (KMAX + 4);
+    static bool attr = false;
+    if (!attr) {
+        ASR_HIP_TRY(hipFuncSetAttribute((const void*)gemm_wide_kernel<BNW, KMAX, EPI>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    const int ncol = (g.N + BNW - 1) / BNW;
+    const int ntile = (g.M + 16 * GW_W - 1) / (16 * GW_W);
+    int rows = ncu / (ncol > 0 ? ncol : 1);
+    rows = rows < ntile ? rows : ntile;
+    rows = rows > 0 ? rows : 1;
+    hipLaunchKernelGGL((gemm_wide_kernel<BNW, KMAX, EPI>), dim3((unsigned)rows, (unsigned)ncol), dim3(64 * GW_W),
+                       lds, s, g);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// ASR_GEMM_WIDE=0: the tiled kernel instead (A/B runs).
+static bool wide_off() {
+    const char* e = getenv("ASR_GEMM_WIDE");
+    return e && e[0] == '0';
+}
+
+// The wide kernel when its shape applies: float4 A rows, row-major B, K <= 256,
+// N >= 128, a tall M (at least 4 tiles per CU so that the slice load amortises).
+template <int EPI>
+static bool try_gemm_wide(const GemmArgs& g, hipStream_t s, int& rc) {
+    if (EPI != EPI_NONE && EPI != EPI_BIAS && EPI != EPI_BIAS_RELU) return false;
+    const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
+    if (!va || g.sbn != 1 || g.N < 128 || g.K > 256 || (long)g.M < 1024L * 128 || wide_off()) return false;
+    rc = launch_gemm_wide_k<128, 256, EPI>(g, s);
+    return true;
+}
+
 // ASR_GEMM_NARROW=0: the tiled kernel for narrow outputs too (A/B runs).
 static bool narrow_off() {
     static const bool off = [] {
@@ -315,6 +446,8 @@ static int launch_gemm_epi(const GemmArgs& g, hipStream_t s) {
     // the A stream as float4 rows: narrow outputs take the LDS-free A path
     const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
     if (EPI != EPI_DUAL_TANH && g.N <= 64 && va && !narrow_off()) return launch_gemm_narrow<EPI>(g, s);
+    int rc;
+    if (try_gemm_wide<EPI>(g, s, rc)) return rc;
     if (g.N <= 32) return launch_gemm_bn<32, EPI>(g, s);
     return launch_gemm_bn<64, EPI>(g, s);
 }

@@ -86,6 +86,34 @@ def test_linear_random(M, K, N, epi):
     close(y.toCpu(), ref.numpy())
 
 
+@pytest.mark.parametrize("M,K,N,epi", [(140000, 256, 256, "none"), (131089, 100, 192, "bias"),
+                                       (262144, 256, 128, "relu"), (135000, 64, 320, "none")])
+def test_linear_wide_persistent(M, K, N, epi, monkeypatch):
+    """Tall-skinny wide GEMMs (M >= 131072, N >= 128, K <= 256: the RNN input
+    projection at C4) take the persistent kernel with B^T resident in LDS;
+    ragged M, partial column slices and K below the slice depth, vs torch
+    fp32; and the tiled kernel (ASR_GEMM_WIDE=0) agrees to fp32 rounding."""
+    rng = np.random.default_rng(M + K + N)
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = (rng.uniform(-1, 1, (K, N)) / np.sqrt(K)).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, N).astype(np.float32)
+    ref = torch.from_numpy(x) @ torch.from_numpy(W)
+    code = {"none": asr.EPI_NONE, "bias": asr.EPI_BIAS, "relu": asr.EPI_BIAS_RELU}[epi]
+    if epi != "none":
+        ref = ref + torch.from_numpy(b)
+    if epi == "relu":
+        ref = torch.relu(ref)
+    dx, dW, db = dm(x), dm(W), dm(b.reshape(N, 1))
+    y = asr.DeviceMatrix(M, N)
+    asr.linear_fwd(dx, dW, db, y, code)
+    got = y.toCpu()
+    close(got, ref.numpy())
+    y2 = asr.DeviceMatrix(M, N)
+    monkeypatch.setenv("ASR_GEMM_WIDE", "0")
+    asr.linear_fwd(dx, dW, db, y2, code)
+    close(y2.toCpu(), got)
+
+
 @pytest.mark.parametrize("M,K,N", [(32000, 256, 29), (100, 64, 5), (77, 30, 64), (300, 1024, 1000), (9, 16, 65)])
 def test_linear_logsoftmax(M, K, N):
     rng = np.random.default_rng(N)
