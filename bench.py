@@ -322,6 +322,11 @@ def main():
                     help="CUs per decode group (0: one per utterance, B rounded up to 8); fewer "
                          "CUs than utterances puts several decode workgroups on a CU when their "
                          "registers allow (--waves 4: 188 VGPRs, one wave per SIMD each)")
+    ap.add_argument("--decode-partition", type=int, default=0,
+                    help="batches that fill the chip: decode streams on CUs [0, N), production on the rest "
+                         "(0: every stream on every CU)")
+    ap.add_argument("--no-partition", action="store_true",
+                    help="batches that fill the chip: decode and production share every CU")
     ap.add_argument("--packed", action="store_true",
                     help="4-wave decode workgroups two to a CU, 5 batches in flight (C2-like shapes)")
     ap.add_argument("--prod-split", default="auto", choices=["auto", "off", "prod", "all", "norec"],
@@ -410,7 +415,8 @@ def main():
     waves = 4 if packed else args.waves
     gcu = min(ncu, args.decode_cus or (-(-B // 16) * 8 if packed else bcu))
     D = 1
-    plain = False   # D decodes share every CU (no CU masks): batches that fill the chip
+    plain = False   # batches that fill the chip: D decodes sharing the decode CUs
+    dpart = args.decode_partition   # decode CUs [0, dpart), production on the rest (0: all shared)
     if pipeline:
         # auto: up to 3 decode groups for H <= 256 (C2: 38.7 M vs 21.1 M frames/s at
         # D = 1), 2 for the H = 1024 recurrence (C5: D = 2 3.48 M, D = 3 2.99 M,
@@ -418,14 +424,23 @@ def main():
         if packed:
             D = max(1, min(5, (ncu - bcu) // gcu))
         elif 2 * bcu > ncu and H <= 256 and V + 1 <= 64 and not args.decode_cus:
-            # A batch fills the chip (C4's shards: 256 utterances per GPU at 8
-            # GPUs).  Consecutive batches then decode concurrently on plain
-            # streams until ~3 utterances share each CU — the library packs
-            # them three 4-wave workgroups to a CU (asr_ctc_set_concurrency);
-            # C4 on one GPU (2048 = 8 per CU) needs no second batch.
+            # A batch fills the chip (C4: 2048 / N utterances per GPU).
+            # Consecutive batches then decode concurrently until ~3 utterances
+            # share each CU — the library packs them three 4-wave workgroups
+            # to a CU (asr_ctc_set_concurrency); C4 on one GPU (2048 = 8 per
+            # CU) needs no second batch.  Up to 4 per CU the production gets
+            # its own CUs (the decodes would otherwise starve it: its GEMM and
+            # recurrence workgroups cannot share a CU with three decode
+            # workgroups), 7/16 of them, with 4 production streams and the
+            # MFMA recurrence (16 utterances per CU; its 4.6 ms latency is
+            # hidden by the 4 streams).  Measured at 256 per GPU
+            # (profiles/r03/): every CU shared 73.2 M frames/s, decode on
+            # 192 / 160 / 144 CUs 63.4 / 82.3 / 86.0 M.
             u = -(-B // ncu)
             D = args.inflight or max(1, -(-3 // u))
-            plain = D > 1
+            plain = True
+            if u <= 4 and not args.no_partition:
+                dpart = args.decode_partition or (ncu * 9 // 16) // 8 * 8
         else:
             D = args.inflight or max(1, min(3 if H <= 256 else 2, ncu // gcu - 1))
         if D > 1 and not plain and (D + 1) * gcu > ncu:
@@ -434,11 +449,13 @@ def main():
     # produced, and a buffer is only produced into after its batch's results
     # were read (asr_amd.h lifetime rule: an overflow retry re-reads it), so
     # D + 1 buffers (--overlap-results, D = 1: a third one).
-    split_prod_auto = D > 1 and H <= 256   # --prod-split auto (below)
+    split_prod_auto = D > 1 and H <= 256 and not plain   # --prod-split auto (below)
     Pn = 1
     if pipeline and not (args.prod_split in ("prod", "all", "norec") or
                          (args.prod_split == "auto" and split_prod_auto)):
-        Pn = args.prod_streams or (2 if D > 1 and H > 256 else 1)
+        Pn = args.prod_streams or (4 if plain and dpart else (2 if D > 1 and H > 256 else 1))
+    if plain and dpart and H <= 256:   # 16 utterances per CU of the production partition
+        asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
     # P production streams produce P batches ahead: D + P buffers
     nbuf = (D + Pn if D > 1 or Pn > 1 else (3 if args.overlap_results else 2)) if pipeline else 1
     d_hid = [asr.DeviceMatrix(T * B, H) for _ in range(nbuf)]
@@ -454,7 +471,11 @@ def main():
         split = args.cu_split
         if plain:
             split = "plain"
-            s_decs = [torch.cuda.Stream() for _ in range(D)]
+            if dpart:   # decodes on CUs [0, dpart), production on [dpart, ncu)
+                s_decs = [cu_range_stream(0, dpart) for _ in range(D)]
+                s_prod = cu_range_stream(dpart, ncu)
+            else:
+                s_decs = [torch.cuda.Stream() for _ in range(D)]
             s_dec = s_decs[0]
         elif D > 1:
             split = "groups"
@@ -465,9 +486,11 @@ def main():
         if split not in ("none", "groups", "plain"):   # the RNN's workgroups then never share a CU with the decoder's
             s_prod, s_dec = cu_masked_streams(split, B)
             s_decs = [s_dec]
-        split_note = {"none": "", "plain": f"; {D} batches decoding at once on plain streams (batch i on stream "
-                                           f"i % {D}), every CU shared, decoders scheduled for {D} x {B} "
-                                           f"utterances (asr_ctc_set_concurrency)",
+        split_note = {"none": "", "plain": f"; {D} batches decoding at once (batch i on stream i % {D}) "
+                                           + (f"on CUs [0, {dpart}), production on the rest"
+                                              if dpart else "on every CU") +
+                                           f", decoders scheduled for {D} x {B} utterances "
+                                           f"(asr_ctc_set_concurrency)",
                       "half": "; decode on CUs [0, n/2), production on [n/2, n)",
                       "fit": f"; decode on CUs [0, {gcu}) (one per utterance), production on the rest",
                       "interleave": "; decode on even CUs, production on odd",
@@ -481,7 +504,7 @@ def main():
         if psplit == "off":
             s_gemm = s_prod
         elif psplit == "all":
-            s_gemm = torch.cuda.Stream()
+            s_gemm = cu_range_stream(dpart, ncu) if split == "plain" and dpart else torch.cuda.Stream()
         elif psplit == "norec" and split == "groups":
             # recurrence on the B CUs after the decode groups (one workgroup per
             # utterance); the GEMMs on every other CU, decode groups included
@@ -498,7 +521,8 @@ def main():
                            f"second stream ({where}) one batch ahead")
         s_prods = [s_prod]
         for _ in range(Pn - 1):   # more production streams on the production CUs
-            s_prods.append(cu_range_stream(D * gcu, ncu) if split == "groups" else torch.cuda.Stream())
+            s_prods.append(cu_range_stream(D * gcu, ncu) if split == "groups" else
+                           cu_range_stream(dpart, ncu) if split == "plain" and dpart else torch.cuda.Stream())
         if Pn > 1:
             split_note += f"; {Pn} production streams, batch i produced on stream i % {Pn}"
         if args.result_stream:   # tracebacks off the decode stream
@@ -756,7 +780,7 @@ def main():
                        f": B={B}/GPU (global {GB}), T={T}, hidden={H}, vocab={V}, beam={beam}",
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
-                       "inflight_decodes": D, "production_streams": Pn,
+                       "inflight_decodes": D, "production_streams": Pn, "decode_partition_cus": dpart or None,
                        "decode_waves": decs[last["k"]].config()[1],   # the schedule the decodes ran
                        "decode_cus_per_batch": gcu if pipeline and D > 1 and not plain else None,
                        "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "

@@ -54,7 +54,7 @@ EXPORTS = [
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
-    "asr_ctc_set_concurrency",
+    "asr_ctc_set_concurrency", "asr_rnn_set_recurrence",
 ]
 
 
@@ -107,6 +107,7 @@ def lib() -> ctypes.CDLL:
         "asr_rnn_cell_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
+        "asr_rnn_set_recurrence": [_i],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -264,6 +265,14 @@ def rnn_bidir_fwd(x: DeviceMatrix, params: Sequence[Tuple[DeviceMatrix, ...]], o
     if stream == 0:
         check(lib().asr_stream_sync(None), "asr_stream_sync")
     return out
+
+
+RNN_RECUR_AUTO, RNN_RECUR_VALU, RNN_RECUR_MFMA = 0, 1, 2
+
+
+def rnn_set_recurrence(kind: int) -> None:
+    """Process-wide recurrence kernel choice (asr_rnn_set_recurrence)."""
+    check(lib().asr_rnn_set_recurrence(int(kind)), "asr_rnn_set_recurrence")
 
 
 def rnn_cell_fwd(x: DeviceMatrix, h_prev: DeviceMatrix, W_ih: DeviceMatrix,

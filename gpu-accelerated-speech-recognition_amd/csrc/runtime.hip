@@ -181,9 +181,13 @@ int asr_rnn_cell_fwd(const float* x, const float* h_prev, const float* W_ih, con
 // kernel ceil(B / 16n) rounds of ~3.7x the step: MFMA from B >= 4n on (and
 // it leaves CUs free for concurrent work well before that).
 // ASR_RNN_MFMA=0/1 forces the choice (A/B timing).
+static std::atomic<int> g_rnn_recur_kind{ASR_RNN_RECUR_AUTO};   // asr_rnn_set_recurrence
+
 static bool rnn_use_mfma(int B, int H) {
     if ((H & 15) != 0) return false;
     if (const char* f = getenv("ASR_RNN_MFMA")) return atoi(f) != 0;
+    const int kind = g_rnn_recur_kind.load(std::memory_order_relaxed);
+    if (kind != ASR_RNN_RECUR_AUTO) return kind == ASR_RNN_RECUR_MFMA;
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
@@ -219,6 +223,12 @@ static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
         }
         if (rc) return rc;
     }
+    return ASR_OK;
+}
+
+int asr_rnn_set_recurrence(int kind) {
+    if (kind != ASR_RNN_RECUR_AUTO && kind != ASR_RNN_RECUR_VALU && kind != ASR_RNN_RECUR_MFMA) return ASR_ERR_ARG;
+    g_rnn_recur_kind.store(kind, std::memory_order_relaxed);
     return ASR_OK;
 }
 

@@ -122,6 +122,17 @@ int asr_rnn_fwd(const float* d_x, const float* d_h0, const float* d_W_ih, const 
 int asr_rnn_recur_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_ih,
                       const float* d_b_hh, float* d_hiddens, int T, int B, int H, asr_stream_t s);
 
+/* Recurrence kernel choice for H <= 256 (H % 16 == 0), process-wide:
+ * ASR_RNN_RECUR_VALU — one utterance per CU, W_hh in registers: the shortest
+ *   step (~0.7-0.9 us), a whole CU per utterance;
+ * ASR_RNN_RECUR_MFMA — 16 utterances per workgroup on MFMA: ~4.6 us per step
+ *   but ~3x less CU time per utterance (for throughput pipelines whose
+ *   production runs beside other work);
+ * ASR_RNN_RECUR_AUTO (default) — MFMA from B >= 4 x CUs on.
+ * Results agree to fp32 rounding (different summation order). */
+enum { ASR_RNN_RECUR_AUTO = 0, ASR_RNN_RECUR_VALU = 1, ASR_RNN_RECUR_MFMA = 2 };
+int asr_rnn_set_recurrence(int kind);
+
 /* Bidirectional single-layer RNN — nn.RNN(bidirectional=True) of the Python
  * baseline (baseline/model.py:30, "bidir true"); the C++
  * RNN class (RNN.h:13-20) has no such mode, so this is an added entry point.
