@@ -431,16 +431,21 @@ def main():
             # CU) needs no second batch.  Up to 4 per CU the production gets
             # its own CUs (the decodes would otherwise starve it: its GEMM and
             # recurrence workgroups cannot share a CU with three decode
-            # workgroups), 7/16 of them, with 4 production streams and the
+            # workgroups), half of them, with 3 production streams and the
             # MFMA recurrence (16 utterances per CU; its 4.6 ms latency is
-            # hidden by the 4 streams).  Measured at 256 per GPU
-            # (profiles/r03/): every CU shared 73.2 M frames/s, decode on
-            # 192 / 160 / 144 CUs 63.4 / 82.3 / 86.0 M.
+            # hidden by the streams), and at least two batches decode at once
+            # (the next batch's workgroups fill the CUs the last round of the
+            # previous one leaves idle).  Measured (profiles/r03/bench_scan.md):
+            # 256 per GPU: every CU shared 73.2 M frames/s, decode on 192 /
+            # 160 / 144 / 128 / 112 CUs 63.4 / 82.3 / 86.0 / 89.3 / 69.2 M;
+            # 1024 per GPU: one decode at a time 79.3 M, two 94.4 M.
             u = -(-B // ncu)
-            D = args.inflight or max(1, -(-3 // u))
             plain = True
             if u <= 4 and not args.no_partition:
-                dpart = args.decode_partition or (ncu * 9 // 16) // 8 * 8
+                dpart = args.decode_partition or (ncu // 2) // 8 * 8
+                D = args.inflight or max(2, -(-3 // u))
+            else:
+                D = args.inflight or max(1, -(-3 // u))
         else:
             D = args.inflight or max(1, min(3 if H <= 256 else 2, ncu // gcu - 1))
         if D > 1 and not plain and (D + 1) * gcu > ncu:
@@ -453,7 +458,7 @@ def main():
     Pn = 1
     if pipeline and not (args.prod_split in ("prod", "all", "norec") or
                          (args.prod_split == "auto" and split_prod_auto)):
-        Pn = args.prod_streams or (4 if plain and dpart else (2 if D > 1 and H > 256 else 1))
+        Pn = args.prod_streams or (3 if plain and dpart else (2 if D > 1 and H > 256 else 1))
     if plain and dpart and H <= 256:   # 16 utterances per CU of the production partition
         asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
     # P production streams produce P batches ahead: D + P buffers
