@@ -122,6 +122,7 @@ def main():
     SIGMAS = [x if x == "bench" else float(x) for x in args.sigmas.split(",")]
     asr.set_device(0)
     ap_cases = {"c2": (500, 64, 29, 50), "c3": (1000, 256, 29, 100),
+                "s64": (300, 64, 29, 50), "s768": (300, 768, 29, 50),   # alone / three per CU
                 "c5": (2000, 32, 1000, 200)}   # C5: 32 utterances per GPU
     ap_cases = [ap_cases[c] for c in args.cases.split(",")]
     for (T, B, V, beam) in ap_cases:
