@@ -341,9 +341,9 @@ def main():
                          "at once (0 = auto: 2 when D > 1 and H > 256, i.e. C5's latency-bound "
                          "per-frame recurrence launches; else 1)")
     ap.add_argument("--graph-production", default="auto", choices=["auto", "on", "off"],
-                    help="capture each buffer's production (RNN + projection: at C5 ~2000 recurrence "
-                         "launches) once in a HIP graph and replay it per batch, so the host no longer "
-                         "queues every launch (auto: on when H > 256 and production is not split)")
+                    help="capture each buffer's whole production (RNN + projection) in a torch CUDA graph "
+                         "and replay it per batch (auto: off; the library already replays C5's ~2000 "
+                         "per-frame recurrence launches from its own HIP graph)")
     ap.add_argument("--result-stream", action="store_true",
                     help="run each batch's traceback on a third stream (measured slower at C2)")
     ap.add_argument("--dry-run-cpu", action="store_true",
@@ -637,8 +637,9 @@ def main():
             collect(pending.pop(0))
 
     graphs = None
-    if pipeline and psplit == "off" and (args.graph_production == "on" or
-                                         (args.graph_production == "auto" and H > 256)):
+    # auto = off: the library replays the per-frame recurrence launches of
+    # H > 256 from its own HIP graph (runtime.hip rnn_recurrence_frames)
+    if pipeline and psplit == "off" and args.graph_production == "on":
         # one HIP graph per buffer (fixed pointers), captured after a first
         # eager production sized every workspace; replayed on the production
         # streams by produce_graph()

@@ -539,15 +539,18 @@ __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict
         pnext = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             __builtin_amdgcn_make_buffer_rsrc(base + tstride, 0, t + 1 < T ? nbytes : 0, RSRC3), voff, 0, 0));
         const float4* hq = reinterpret_cast<const float4*>(&hs[cur][q * RNN_QS]);
-        float acc = 0.f;
+        // four independent FMA chains (16 deep instead of 64): the step is a
+        // dependent-latency chain at one utterance per CU
+        float a4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i4 = 0; i4 < 16; i4++) {
             const float4 h4 = hq[i4];
-            acc = fmaf(h4.x, w[4 * i4 + 0], acc);
-            acc = fmaf(h4.y, w[4 * i4 + 1], acc);
-            acc = fmaf(h4.z, w[4 * i4 + 2], acc);
-            acc = fmaf(h4.w, w[4 * i4 + 3], acc);
+            a4[0] = fmaf(h4.x, w[4 * i4 + 0], a4[0]);
+            a4[1] = fmaf(h4.y, w[4 * i4 + 1], a4[1]);
+            a4[2] = fmaf(h4.z, w[4 * i4 + 2], a4[2]);
+            a4[3] = fmaf(h4.w, w[4 * i4 + 3], a4[3]);
         }
+        float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
         const float h = tanhf((p + acc) + bias);

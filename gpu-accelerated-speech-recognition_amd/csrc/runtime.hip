@@ -197,16 +197,100 @@ static bool rnn_use_mfma(int B, int H) {
 
 // Recurrence over a hid buffer that already holds the input projection
 // P_t = x_t . W_ih, in place: hid[t] = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)).
+static int rnn_frames_eager(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
+                            float* hid, int T, int B, int H, hipStream_t st);
+
+// The T per-frame launches of a (pointers, shape) recurrence, captured once
+// into a HIP graph and replayed: the host then queues one graph launch per
+// sequence instead of T kernel launches (C5: 2,000 per batch, BL: 200), and
+// the device runs them back to back.  Captured at the second call with the
+// same key (a one-off call runs eagerly), replayed on the caller's stream;
+// never inside the caller's own stream capture (then the launches are
+// captured into that graph as they are).  A small cache, evicting the least
+// recently used.  ASR_RNN_GRAPH=0: always eager (A/B).
+struct RecurGraphKey {
+    int dev, T, B, H;
+    const void *h0, *W_hh, *b_ih, *b_hh, *hid;
+    bool operator==(const RecurGraphKey& o) const {
+        return dev == o.dev && T == o.T && B == o.B && H == o.H && h0 == o.h0 && W_hh == o.W_hh &&
+               b_ih == o.b_ih && b_hh == o.b_hh && hid == o.hid;
+    }
+};
+struct RecurGraph {
+    RecurGraphKey key;
+    int uses = 0;
+    hipGraphExec_t exec = nullptr;
+    unsigned long last = 0;
+};
+static std::mutex g_graph_mu;
+static std::vector<RecurGraph> g_graphs;
+static unsigned long g_graph_tick = 0;
+constexpr size_t RECUR_GRAPH_CACHE = 8;
+
+static int rnn_recurrence_frames(const float* h0, const float* W_hh, const float* b_ih,
+                                 const float* b_hh, float* hid, int T, int B, int H, hipStream_t st) {
+    const char* ge = getenv("ASR_RNN_GRAPH");
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if ((ge && ge[0] == '0') || T < 8 || hipStreamIsCapturing(st, &cap) != hipSuccess ||
+        cap != hipStreamCaptureStatusNone)
+        return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+    RecurGraphKey key{0, T, B, H, h0, W_hh, b_ih, b_hh, hid};
+    ASR_HIP_TRY(hipGetDevice(&key.dev));
+    std::lock_guard<std::mutex> lock(g_graph_mu);
+    RecurGraph* e = nullptr;
+    for (auto& g : g_graphs)
+        if (g.key == key) e = &g;
+    if (!e) {
+        if (g_graphs.size() >= RECUR_GRAPH_CACHE) {   // evict the least recently used
+            auto lru = std::min_element(g_graphs.begin(), g_graphs.end(),
+                                        [](const RecurGraph& a, const RecurGraph& b) { return a.last < b.last; });
+            if (lru->exec) hipGraphExecDestroy(lru->exec);
+            g_graphs.erase(lru);
+        }
+        g_graphs.push_back(RecurGraph{key});
+        e = &g_graphs.back();
+    }
+    e->last = ++g_graph_tick;
+    if (++e->uses < 2 && !e->exec)   // first use: eager (kernel attributes set, nothing captured for one-offs)
+        return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+    if (!e->exec) {
+        hipStream_t cs;
+        ASR_HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        hipGraph_t graph = nullptr;
+        int rc = ASR_OK;
+        hipError_t he = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+        if (he == hipSuccess) {
+            rc = rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, cs);
+            he = hipStreamEndCapture(cs, &graph);
+        }
+        if (he == hipSuccess && rc == ASR_OK) he = hipGraphInstantiate(&e->exec, graph, nullptr, nullptr, 0);
+        if (graph) hipGraphDestroy(graph);
+        hipStreamDestroy(cs);
+        if (rc) return rc;
+        if (he != hipSuccess) {   // no graph: stay eager for this key
+            e->exec = nullptr;
+            return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+        }
+    }
+    ASR_HIP_TRY(hipGraphLaunch(e->exec, st));
+    return ASR_OK;
+}
+
 static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
                           const float* b_hh, float* hid, int T, int B, int H, hipStream_t st) {
-    int rc = ASR_OK;
     if (H <= 256) {
         if (rnn_use_mfma(B, H)) return asr::rnn_recur_mfma_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
         return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
     }
-    // H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
-    // h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
-    // H % 128 == 0, else the VALU kernel with W_hh slices in LDS.
+    return rnn_recurrence_frames(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+}
+
+// H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
+// h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
+// H % 128 == 0, else the VALU kernel with W_hh slices in LDS.
+static int rnn_frames_eager(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
+                            float* hid, int T, int B, int H, hipStream_t st) {
+    int rc = ASR_OK;
     for (int t = 0; t < T; t++) {
         float* ht = hid + (size_t)t * B * H;
         const float* hp = t == 0 ? h0 : hid + (size_t)(t - 1) * B * H;

@@ -387,3 +387,32 @@ def test_rnn_forward_h2048():
     asr.rnn_fwd(dm(x), dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B,
                 h0=dm(h0))
     close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
+
+
+def test_rnn_h_gt_256_graph_replay(monkeypatch):
+    """H > 256: the per-frame recurrence launches are captured once into a
+    library-owned HIP graph (second call with the same pointers and shape)
+    and replayed; eager (ASR_RNN_GRAPH=0), first, replayed and re-replayed
+    calls give the same bits, and agree with torch."""
+    T, B, I, H = 24, 40, 64, 512
+    rng = np.random.default_rng(512)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    W = [dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1))]
+    dx, dh0 = dm(x), dm(h0)
+    hid = asr.DeviceMatrix(T * B, H)
+    outs = []
+    for _ in range(3):
+        asr.rnn_fwd(dx, *W, hid, T, B, h0=dh0)
+        outs.append(hid.toCpu())
+    monkeypatch.setenv("ASR_RNN_GRAPH", "0")
+    asr.rnn_fwd(dx, *W, hid, T, B, h0=dh0)
+    outs.append(hid.toCpu())
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    close(outs[0], _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
