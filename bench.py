@@ -459,7 +459,10 @@ def main():
     if pipeline and not (args.prod_split in ("prod", "all", "norec") or
                          (args.prod_split == "auto" and split_prod_auto)):
         Pn = args.prod_streams or (3 if plain and dpart else (2 if D > 1 and H > 256 else 1))
-    if plain and dpart and H <= 256:   # 16 utterances per CU of the production partition
+    if plain and H <= 256:
+        # 16 utterances per CU (the production partition's, or beside the
+        # decodes), and the same recurrence kernel at every shard size, so
+        # that an utterance's emissions are the same bits at N = 1 / 2 / 4 / 8
         asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
     # P production streams produce P batches ahead: D + P buffers
     nbuf = (D + Pn if D > 1 or Pn > 1 else (3 if args.overlap_results else 2)) if pipeline else 1

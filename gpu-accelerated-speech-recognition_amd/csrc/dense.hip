@@ -392,12 +392,15 @@ static bool wide_off() {
 }
 
 // The wide kernel when its shape applies: float4 A rows, row-major B, K <= 256,
-// N >= 128, a tall M (at least 4 tiles per CU so that the slice load amortises).
+// N >= 128 — whatever M, so that a row's result never depends on how many
+// rows share the call (the RNN input projection of an utterance is the same
+// bits in a 2048-utterance batch and in any shard of it: utterance sharding
+// over GPUs relies on that).
 template <int EPI>
 static bool try_gemm_wide(const GemmArgs& g, hipStream_t s, int& rc) {
     if (EPI != EPI_NONE && EPI != EPI_BIAS && EPI != EPI_BIAS_RELU) return false;
     const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
-    if (!va || g.sbn != 1 || g.N < 128 || g.K > 256 || (long)g.M < 1024L * 128 || wide_off()) return false;
+    if (!va || g.sbn != 1 || g.N < 128 || g.K > 256 || wide_off()) return false;
     rc = launch_gemm_wide_k<128, 256, EPI>(g, s);
     return true;
 }
