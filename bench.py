@@ -414,6 +414,8 @@ def main():
               and H <= 256 and V + 1 <= 64 and 4 * bcu <= ncu)
     waves = 4 if packed else args.waves
     gcu = min(ncu, args.decode_cus or (-(-B // 16) * 8 if packed else bcu))
+    Kb = beam + 1   # the library's automatic beam capacity (runtime.hip asr_ctc_create)
+    kcap = -(-(Kb + max(8, Kb // 8)) // 32) * 32   # > 64 (C3's beam 100): no 3-per-CU 4-wave kernel
     D = 1
     plain = False   # batches that fill the chip: D decodes sharing the decode CUs
     dpart = args.decode_partition   # decode CUs [0, dpart), production on the rest (0: all shared)
@@ -423,7 +425,7 @@ def main():
         # gpurun_out/r2g31); packed: 5 (one recurrence group of bcu CUs beside them)
         if packed:
             D = max(1, min(5, (ncu - bcu) // gcu))
-        elif 2 * bcu > ncu and H <= 256 and V + 1 <= 64 and not args.decode_cus:
+        elif 2 * bcu > ncu and H <= 256 and V + 1 <= 64 and kcap <= 64 and not args.decode_cus:
             # A batch fills the chip (C4: 2048 / N utterances per GPU).
             # Consecutive batches then decode concurrently until ~3 utterances
             # share each CU — the library packs them three 4-wave workgroups

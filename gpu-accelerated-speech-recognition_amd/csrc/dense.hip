@@ -104,12 +104,17 @@ __device__ __forceinline__ void mma_tile(Tile<BN, BK>& L, const float* __restric
         }
         __syncthreads();
         if (k0 + BK < K) load(k0 + BK);   // next stage in flight during the MFMAs
+        // MFMA step kk = 4c + e of lane group g contracts k = 16c + 4g + e —
+        // the k order of the narrow and wide kernels, so every GEMM path
+        // accumulates a row in the same sequence and gives the same bits
+        // (a row's result never depends on which kernel its call took)
 #pragma unroll
         for (int kk = 0; kk < BK / 4; kk++) {
-            const float af = L.As[(w * 16 + (lane & 15)) * AST + kk * 4 + (lane >> 4)];
+            const int ko = 16 * (kk >> 2) + 4 * (lane >> 4) + (kk & 3);
+            const float af = L.As[(w * 16 + (lane & 15)) * AST + ko];
 #pragma unroll
             for (int nt = 0; nt < BN / 16; nt++) {
-                const float bf = L.Bs[(kk * 4 + (lane >> 4)) * BST + nt * 16 + (lane & 15)];
+                const float bf = L.Bs[ko * BST + nt * 16 + (lane & 15)];
                 acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, bf, acc[nt], 0, 0, 0);
             }
         }
@@ -392,15 +397,16 @@ static bool wide_off() {
 }
 
 // The wide kernel when its shape applies: float4 A rows, row-major B, K <= 256,
-// N >= 128 — whatever M, so that a row's result never depends on how many
-// rows share the call (the RNN input projection of an utterance is the same
-// bits in a 2048-utterance batch and in any shard of it: utterance sharding
-// over GPUs relies on that).
+// N >= 128, a tall M (at least 4 tiles per CU so that the slice load
+// amortises; C2's 32,000 rows: 62 us wide vs 50 us tiled).  Both kernels
+// accumulate in the same k order, so the choice never changes a row's bits
+// (an utterance's input projection is the same in a 2048-utterance batch
+// and in any shard of it: utterance sharding over GPUs relies on that).
 template <int EPI>
 static bool try_gemm_wide(const GemmArgs& g, hipStream_t s, int& rc) {
     if (EPI != EPI_NONE && EPI != EPI_BIAS && EPI != EPI_BIAS_RELU) return false;
     const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
-    if (!va || g.sbn != 1 || g.N < 128 || g.K > 256 || wide_off()) return false;
+    if (!va || g.sbn != 1 || g.N < 128 || g.K > 256 || (long)g.M < 1024L * 128 || wide_off()) return false;
     rc = launch_gemm_wide_k<128, 256, EPI>(g, s);
     return true;
 }
@@ -542,18 +548,17 @@ __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict
         pnext = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             __builtin_amdgcn_make_buffer_rsrc(base + tstride, 0, t + 1 < T ? nbytes : 0, RSRC3), voff, 0, 0));
         const float4* hq = reinterpret_cast<const float4*>(&hs[cur][q * RNN_QS]);
-        // four independent FMA chains (16 deep instead of 64): the step is a
-        // dependent-latency chain at one utterance per CU
-        float a4[4] = {0.f, 0.f, 0.f, 0.f};
+        // one FMA chain: four independent chains measured slower (C2
+        // recurrence 0.35 -> 0.46 ms, gpurun_out/r3m)
+        float acc = 0.f;
 #pragma unroll
         for (int i4 = 0; i4 < 16; i4++) {
             const float4 h4 = hq[i4];
-            a4[0] = fmaf(h4.x, w[4 * i4 + 0], a4[0]);
-            a4[1] = fmaf(h4.y, w[4 * i4 + 1], a4[1]);
-            a4[2] = fmaf(h4.z, w[4 * i4 + 2], a4[2]);
-            a4[3] = fmaf(h4.w, w[4 * i4 + 3], a4[3]);
+            acc = fmaf(h4.x, w[4 * i4 + 0], acc);
+            acc = fmaf(h4.y, w[4 * i4 + 1], acc);
+            acc = fmaf(h4.z, w[4 * i4 + 2], acc);
+            acc = fmaf(h4.w, w[4 * i4 + 3], acc);
         }
-        float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
         const float h = tanhf((p + acc) + bias);
