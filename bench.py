@@ -325,6 +325,9 @@ def main():
     ap.add_argument("--decode-partition", type=int, default=0,
                     help="batches that fill the chip: decode streams on CUs [0, N), production on the rest "
                          "(0: every stream on every CU)")
+    ap.add_argument("--py-pipeline", action="store_true",
+                    help="the round-2 Python orchestration over torch streams instead of the library's "
+                         "native pipeline (asr_pipeline_*); implied by its Python-only knobs")
     ap.add_argument("--no-partition", action="store_true",
                     help="batches that fill the chip: decode and production share every CU")
     ap.add_argument("--packed", action="store_true",
@@ -402,6 +405,13 @@ def main():
     d_x = DM(make_features(T, B, In, first))
     pipeline = not args.no_pipeline and not args.decode_only
     ncu = torch.cuda.get_device_properties(local).multi_processor_count if torch is not None else 256
+    # the library's native pipeline unless a knob of the Python orchestration is asked for
+    native = (pipeline and not args.py_pipeline and not (args.packed or args.decode_cus or args.waves or
+              args.result_stream or args.overlap_results) and args.prod_split == "auto" and
+              args.graph_production != "on" and args.cu_split == "auto")
+    if native:
+        return main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
+                           [d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout])
     bcu = -(-B // 8) * 8   # CUs of one workgroup per utterance
     # --packed (C2-like shapes: H <= 256, V <= 63, a batch on at most a
     # quarter of the CUs): 4-wave decode workgroups (188 VGPRs, one wave per
@@ -711,8 +721,29 @@ def main():
     if world > 1:
         dist.barrier()
 
+    finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
+           decs[last["k"]].best_arrays(), decs[last["k"]].config(),
+           [d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], d_hid[0], d_emis[0], d_emis[last["k"]],
+           {"inflight_decodes": D, "production_streams": Pn, "decode_partition_cus": dpart or None,
+            "decode_cus_per_batch": gcu if pipeline and D > 1 and not plain else None,
+            "pipeline": ("python orchestration over torch streams (--py-pipeline): RNN+projection of "
+                         "batch i+1 on one HIP stream || decode of batch i on another" + split_note +
+                         ("; tracebacks on a third stream" if args.result_stream else "")
+                         if pipeline else "none (sequential)")})
+    for d in decs:
+        d.close()
+    asr.synchronize()
+    destroy_raw_streams()
+
+
+def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms, best,
+           dec_config, weights, d_hid0, d_emis0, d_emis_last, sched):
+    """Everything after the timed region: host gather of the hypotheses,
+    roofline, GEMM MFMA utilisation, CPU baseline and the JSON line (rank 0)."""
+    d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout = weights
+    DM = asr.DeviceMatrix.from_numpy
     # ---- host-side gather of the hypotheses (outside the timed region)
-    labels, lens, lp = decs[last["k"]].best_arrays()
+    labels, lens, lp = best
     records = gather_hypotheses(pack_hypotheses(first, labels, lens, lp), world, rank)
     gather = None
     if rank == 0:
@@ -747,7 +778,7 @@ def main():
     roof = None
     if avg_kernel_ms:
         achieved = bpf * B * T / (avg_kernel_ms * 1e-3) / 1e9
-        ms_, waves_run, _ = decs[last["k"]].config()
+        ms_, waves_run, _ = dec_config
         variant = decoder_variant(V, waves_run, ms_)
         wl = args.config + (" decode-only" if args.decode_only else "")
         traffic = load_counters("traffic", wl, variant)
@@ -769,12 +800,11 @@ def main():
 
     mfma = None
     if rank == 0 and world == 1 and not args.decode_only:
-        mfma = measure_gemms(asr, d_x, d_wih, d_hid[0], d_wout, d_bout, d_emis[0], T, B, In, H, V)
+        mfma = measure_gemms(asr, d_x, d_wih, d_hid0, d_wout, d_bout, d_emis0, T, B, In, H, V)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam,
-                           d_emis[last["k"]])
+        cpu = cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam, d_emis_last)
 
     if rank == 0:
         line = {
@@ -791,22 +821,81 @@ def main():
                        f": B={B}/GPU (global {GB}), T={T}, hidden={H}, vocab={V}, beam={beam}",
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
-                       "inflight_decodes": D, "production_streams": Pn, "decode_partition_cus": dpart or None,
-                       "decode_waves": decs[last["k"]].config()[1],   # the schedule the decodes ran
-                       "decode_cus_per_batch": gcu if pipeline and D > 1 and not plain else None,
-                       "pipeline": ("RNN+projection of batch i+1 on one HIP stream || decode of batch i "
-                                    "on another" + split_note +
-                                    ("; tracebacks on a third stream" if args.result_stream else "")
-                                    if pipeline else "none (sequential)")},
+                       "decode_waves": dec_config[1],   # the schedule the decodes ran
+                       **sched},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "gather": gather,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    for d in decs:
-        d.close()
+
+
+def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, weights):
+    """The default pipelined bench: the library's own throughput pipeline
+    (asr_pipeline_*: streams, buffers, CU placement and decoder schedule chosen
+    natively from the shapes), the host loop only submitting batches and
+    reading each batch's results once `inflight` newer ones are queued."""
+    d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout = weights
+    dcus = -1 if args.no_partition else args.decode_partition
+    pl = asr.Pipeline(T, B, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
+                      inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus)
+    desc = pl.describe()
+    if desc["mode"] == asr.PIPELINE_MODES[1] and H <= 256:
+        # the pipeline's MFMA recurrence for chip-filling batches, also for
+        # the 1-GPU re-decode that checks the gathered shards
+        asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
+    lag = desc["inflight"]
+    kernel_ms = []
+    best = {}
+
+    def take():
+        lab, ln, lp, ms = pl.collect()
+        kernel_ms.append(ms)
+        best["arrays"] = (lab, ln, lp)
+
+    def run(n):
+        for _ in range(n):
+            pl.submit(d_x)
+            while pl.pending() > lag:
+                take()
+        while pl.pending():
+            take()
+
+    run(2 * (desc["inflight"] + desc["prod_streams"]) + 1)   # every buffer, stream and workspace once
+    run(args.warmup)
+    kernel_ms.clear()
+    if world > 1:
+        dist.barrier()
+    gc.collect()
+    gc.disable()
     asr.synchronize()
-    destroy_raw_streams()
+    t0 = time.perf_counter()
+    run(args.steps)
+    asr.synchronize()
+    elapsed = time.perf_counter() - t0
+    gc.enable()
+    elapsed = reduce_max_over_ranks(elapsed, world)
+    if world > 1:
+        dist.barrier()
+    desc = pl.describe()
+    lab, ln, lp = (a.copy() for a in best["arrays"])
+    Kb = beam + 1
+    kcap = -(-(Kb + max(8, Kb // 8)) // 32) * 32
+    # buffers for the GEMM timing and one batch's real emissions for the CPU baseline
+    hid0, em0 = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, V)
+    em_real = asr.DeviceMatrix(T * B, V)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        asr.rnn_fwd(d_x, d_wih, d_whh, d_bih, d_bhh, hid0, T, B)
+        asr.linear_fwd(hid0, d_wout, d_bout, em_real, asr.EPI_BIAS_LOGSOFTMAX)
+    finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
+           (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_real,
+           {"inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
+            "decode_cus": desc["decode_cus"],
+            "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
+                        f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
+                        f"library-owned streams, buffers and decoder schedule"})
+    pl.close()
+    asr.synchronize()
 
 
 def greedy_host(T, V, first, count, seed=20261015):

@@ -55,6 +55,8 @@ EXPORTS = [
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
     "asr_ctc_set_concurrency", "asr_rnn_set_recurrence",
+    "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
+    "asr_pipeline_describe", "asr_pipeline_destroy",
 ]
 
 
@@ -108,6 +110,13 @@ def lib() -> ctypes.CDLL:
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_set_recurrence": [_i],
+        "asr_pipeline_create": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)],
+        "asr_pipeline_submit": [_vp, _vp],
+        "asr_pipeline_collect": [_vp, _vp, _i, _vp, _vp, _vp],
+        "asr_pipeline_pending": [_vp, ctypes.POINTER(_i)],
+        "asr_pipeline_describe": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
+                                  ctypes.POINTER(_i)],
+        "asr_pipeline_destroy": [_vp],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -462,6 +471,70 @@ class CTCDecoder:
     def close(self) -> None:
         if getattr(self, "h", None):
             lib().asr_ctc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PipelineConfig(ctypes.Structure):
+    """asr_pipeline_config (include/asr_amd.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in ("T", "B", "in_", "H", "V", "beam", "blank", "inflight",
+                                           "prod_streams", "decode_cus")]
+
+
+PIPELINE_MODES = {0: "CU groups (small batches)", 1: "chip-filling batches", 2: "CU groups (H > 256)"}
+
+
+class Pipeline:
+    """asr_pipeline_*: RNN -> Linear + log_softmax -> CTC decode over a stream of
+    equal-shape batches, the library overlapping production and decodes on its
+    own streams.  submit(x) queues a batch (features stay valid until its
+    results are collected); collect() returns the oldest batch's
+    (labels [B][T], lengths [B], logp [B], decode_ms)."""
+
+    def __init__(self, T: int, B: int, inp: int, H: int, V: int, beam: int, weights, blank: int = 0,
+                 inflight: int = 0, prod_streams: int = 0, decode_cus: int = 0):
+        self.T, self.B = T, B
+        self.cfg = PipelineConfig(T, B, inp, H, V, beam, blank, inflight, prod_streams, decode_cus)
+        self._w = weights   # (W_ih, W_hh, b_ih, b_hh, W_out, b_out) DeviceMatrix: kept alive
+        h = _vp()
+        check(lib().asr_pipeline_create(ctypes.byref(self.cfg), *[w.ptr for w in weights], ctypes.byref(h)),
+              "asr_pipeline_create")
+        self.h = h.value
+        self._lab = np.zeros((B, max(T, 1)), np.int32)
+        self._len = np.zeros(B, np.int32)
+        self._lp = np.zeros(B, np.float64)
+
+    def describe(self):
+        m, d, p, c, w = _i(), _i(), _i(), _i(), _i()
+        check(lib().asr_pipeline_describe(self.h, ctypes.byref(m), ctypes.byref(d), ctypes.byref(p),
+                                          ctypes.byref(c), ctypes.byref(w)), "asr_pipeline_describe")
+        return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
+                "decode_cus": c.value, "decode_waves": w.value}
+
+    def submit(self, x: "DeviceMatrix") -> None:
+        check(lib().asr_pipeline_submit(self.h, x.ptr), "asr_pipeline_submit")
+
+    def pending(self) -> int:
+        n = _i()
+        check(lib().asr_pipeline_pending(self.h, ctypes.byref(n)), "asr_pipeline_pending")
+        return n.value
+
+    def collect(self):
+        """(labels [B][T] int32, lengths [B], logp [B] fp64, decode_ms) of the
+        oldest batch; the arrays are reused by the next call."""
+        ms = _f()
+        check(lib().asr_pipeline_collect(self.h, _ptr(self._lab), self._lab.shape[1], _ptr(self._len),
+                                         _ptr(self._lp), ctypes.byref(ms)), "asr_pipeline_collect")
+        return self._lab, self._len, self._lp, ms.value
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().asr_pipeline_destroy(self.h)
             self.h = None
 
     def __del__(self):

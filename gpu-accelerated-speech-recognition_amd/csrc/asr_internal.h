@@ -28,6 +28,11 @@ void asr_internal_set_error(const char* what, const char* msg, const char* file,
 
 static inline hipStream_t asr_stream(asr_stream_t s) { return (hipStream_t)s; }
 
+// Recurrence kernel for this thread's next RNN calls (ASR_RNN_RECUR_*; -1:
+// the process-wide asr_rnn_set_recurrence choice).  Set by the pipeline
+// around its production so that it never changes the process-wide state.
+extern thread_local int asr_internal_rnn_kind;
+
 // Order-preserving bijection fp64 <-> u64: a < b  <=>  key(a) < key(b).
 // -0.0 is folded onto +0.0 (they compare equal as doubles).  Key 0 is never
 // produced for a non-NaN value (-inf maps to 0x000FFFFFFFFFFFFF), so it marks

@@ -1,0 +1,360 @@
+// ============================================================================
+// Native throughput pipeline (asr_pipeline_*, include/asr_amd.h): the hot
+// path RNN (input projection + recurrence) -> Linear + log_softmax -> CTC
+// beam search over a stream of equal-shape batches, with the production of
+// later batches overlapped with the decodes of earlier ones on library-owned
+// HIP streams.  The reference runs one batch at a time on the default stream
+// with host syncs between every call (main.cpp:40-72, RNN.cu:9-30,
+// CTCBeamSearch.cu:262-312); a decode is sequential in T and one batch
+// leaves most CUs idle or starves its own production, so throughput needs
+// several batches in flight and a placement of the kernels on the CUs.
+//
+// Schedules (chosen from the shapes):
+//   GROUPS  small batches (<= 1/4 of the CUs at one decode workgroup per
+//           utterance, H <= 256; C2): D = 3 decode streams, each restricted
+//           to its own group of CUs (one workgroup per utterance), the
+//           recurrence on the remaining CUs, the input / emission GEMMs on a
+//           stream over every CU, the input projection issued one batch
+//           ahead so that it overlaps the previous batch's recurrence.
+//   SHARED  batches that fill the chip (H <= 256, beam capacity <= 64; C4's
+//           shards): with <= 4 utterances per CU the decodes get half of the
+//           CUs and D >= 2 batches decode there at once (the decoder packs
+//           three 4-wave workgroups per CU: asr_ctc_set_concurrency), the
+//           production the other half on 3 streams with the MFMA
+//           recurrence; with more utterances per CU everything shares every
+//           CU, one decode at a time.
+//   GROUPS2 H > 256 (C5: 2000 per-frame recurrence launches, replayed from
+//           the library's HIP graph): D = 2 decode groups, 2 production
+//           streams on the remaining CUs.
+// Results come back in submission order (asr_pipeline_collect).  A batch's
+// buffers are reused only after its results were fetched (the decoder's
+// overflow retry re-reads its emissions): submit collects internally when
+// the caller is nbuf batches behind.
+// ============================================================================
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <vector>
+
+#include "asr_internal.h"
+
+namespace {
+
+enum Mode { GROUPS = 0, SHARED = 1, GROUPS2 = 2 };
+
+struct Result {
+    std::vector<int32_t> lab, len;
+    std::vector<double> lp;
+    float ms = 0.f;
+    int rc = ASR_OK;
+};
+
+}  // namespace
+
+struct asr_pipeline {
+    asr_pipeline_config cfg{};
+    const float *W_ih = nullptr, *W_hh = nullptr, *b_ih = nullptr, *b_hh = nullptr;
+    const float *W_out = nullptr, *b_out = nullptr;
+    int ncu = 0, mode = SHARED, D = 1, P = 1, nbuf = 2, gcu = 0, dcus = 0, rnn_kind = -1;
+    bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
+    std::vector<float*> hid, emis;
+    std::vector<asr_ctc_t*> dec;
+    std::vector<hipStream_t> s_dec, s_prod;
+    hipStream_t s_gemm = nullptr;
+    std::vector<hipEvent_t> ev_ready, ev_free, ev_proj, ev_rec;
+    long submitted = 0, decoded = 0, collected = 0;
+    long pending_tail = -1;   // split production: batch whose emission GEMM and decode are not queued yet
+    std::deque<Result> stash;
+};
+
+namespace {
+
+int cu_stream(hipStream_t* s, int ncu, int lo, int hi) {
+    if (lo <= 0 && hi >= ncu) {
+        ASR_HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+        return ASR_OK;
+    }
+    const int words = (ncu + 31) / 32;
+    std::vector<uint32_t> m(words, 0u);
+    for (int c = std::max(0, lo); c < std::min(ncu, hi); c++) m[c / 32] |= 1u << (c % 32);
+    ASR_HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)words, m.data()));
+    return ASR_OK;
+}
+
+// Production of batch i into buffer k (unsplit): RNN forward + emission projection.
+int produce_full(asr_pipeline* p, long i, const float* x) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    hipStream_t sp = p->s_prod[i % p->P];
+    ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    asr_internal_rnn_kind = p->rnn_kind;
+    int rc = asr_rnn_fwd(x, nullptr, p->W_ih, p->W_hh, p->b_ih, p->b_hh, p->hid[k], c.T, c.B, c.in, c.H, sp);
+    asr_internal_rnn_kind = -1;
+    if (!rc) rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
+                                 ASR_EPI_BIAS_LOGSOFTMAX, sp);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
+    return ASR_OK;
+}
+
+// Split production, part 1: input projection on the GEMM stream, recurrence
+// on the recurrence stream.
+int produce_head(asr_pipeline* p, long i, const float* x) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    int rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], c.T * c.B, c.in, c.H, ASR_EPI_NONE, p->s_gemm);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gemm));
+    ASR_HIP_TRY(hipStreamWaitEvent(p->s_prod[0], p->ev_proj[k], 0));
+    asr_internal_rnn_kind = p->rnn_kind;
+    rc = asr_rnn_recur_fwd(nullptr, p->W_hh, p->b_ih, p->b_hh, p->hid[k], c.T, c.B, c.H, p->s_prod[0]);
+    asr_internal_rnn_kind = -1;
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(p->ev_rec[k], p->s_prod[0]));
+    return ASR_OK;
+}
+
+// Split production, part 2: emission projection once the recurrence is done
+// and the previous decode of this buffer has finished.
+int produce_tail(asr_pipeline* p, long i) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_rec[k], 0));
+    ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_free[k], 0));
+    int rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
+                            ASR_EPI_BIAS_LOGSOFTMAX, p->s_gemm);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], p->s_gemm));
+    return ASR_OK;
+}
+
+int enqueue_decode(asr_pipeline* p, long i) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    hipStream_t sd = p->s_dec[i % p->D];
+    ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_ready[k], 0));
+    int rc = asr_ctc_decode(p->dec[k], p->emis[k], c.T, c.B, 1, sd);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(p->ev_free[k], sd));
+    p->decoded = i + 1;
+    return ASR_OK;
+}
+
+// Queue the emission GEMM and decode of the batch whose production was split.
+int flush_tail(asr_pipeline* p) {
+    if (p->pending_tail < 0) return ASR_OK;
+    const long j = p->pending_tail;
+    p->pending_tail = -1;
+    int rc = produce_tail(p, j);
+    if (!rc) rc = enqueue_decode(p, j);
+    return rc;
+}
+
+// Fetch the results of the oldest uncollected batch (blocking).
+int fetch(asr_pipeline* p, Result& r) {
+    const auto& c = p->cfg;
+    const long j = p->collected;
+    if (j >= p->submitted) return ASR_ERR_STATE;
+    if (j >= p->decoded) {
+        int rc = flush_tail(p);
+        if (rc) return rc;
+    }
+    asr_ctc_t* h = p->dec[j % p->nbuf];
+    r.lab.assign((size_t)c.B * c.T, 0);
+    r.len.assign(c.B, 0);
+    r.lp.assign(c.B, 0.0);
+    r.rc = asr_ctc_get_best(h, r.lab.data(), c.T, r.len.data(), r.lp.data());
+    if (r.rc != ASR_OK && r.rc != ASR_ERR_BEAM_OVERFLOW) return r.rc;
+    asr_ctc_last_kernel_ms(h, &r.ms);
+    p->collected = j + 1;
+    return ASR_OK;
+}
+
+void release(asr_pipeline* p) {
+    for (auto s : p->s_dec) if (s) hipStreamSynchronize(s);
+    for (auto s : p->s_prod) if (s) hipStreamSynchronize(s);
+    if (p->s_gemm) hipStreamSynchronize(p->s_gemm);
+    for (auto h : p->dec) asr_ctc_destroy(h);
+    for (auto b : p->hid) hipFree(b);
+    for (auto b : p->emis) hipFree(b);
+    for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec})
+        for (auto e : *v) if (e) hipEventDestroy(e);
+    for (auto s : p->s_dec) if (s) hipStreamDestroy(s);
+    for (auto s : p->s_prod) if (s) hipStreamDestroy(s);
+    if (p->s_gemm) hipStreamDestroy(p->s_gemm);
+}
+
+}  // namespace
+
+extern "C" {
+
+int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const float* W_hh,
+                        const float* b_ih, const float* b_hh, const float* W_out, const float* b_out,
+                        asr_pipeline_t** out) {
+    if (!cfg || !out || !W_ih || !W_hh || !b_ih || !b_hh || !W_out || !b_out) return ASR_ERR_ARG;
+    *out = nullptr;
+    const auto& c = *cfg;
+    if (c.T < 1 || c.B < 1 || c.in < 1 || c.H < 1 || c.V < 2 || c.beam < 1 || c.blank < 0 || c.blank >= c.V ||
+        c.inflight < 0 || c.prod_streams < 0 || c.decode_cus < -1)
+        return ASR_ERR_ARG;
+    asr_pipeline* p = new asr_pipeline();
+    p->cfg = c;
+    p->W_ih = W_ih; p->W_hh = W_hh; p->b_ih = b_ih; p->b_hh = b_hh; p->W_out = W_out; p->b_out = b_out;
+    int dev = 0;
+    int rc = ASR_OK;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || p->ncu < 8) {
+        delete p;
+        return ASR_ERR_HIP;
+    }
+    const int ncu = p->ncu;
+    // the decoder's beam capacity (asr_ctc_create's automatic max_states)
+    const int K = c.beam + 1;
+    const int kcap = (K + std::max(8, K / 8) + 31) / 32 * 32;
+    const int bcu = (c.B + 7) / 8 * 8;   // CUs at one decode workgroup per utterance
+    const int u = (c.B + ncu - 1) / ncu;  // utterances per CU
+    if (c.H <= 256 && c.V + 1 <= 64 && 4 * bcu <= ncu) {
+        p->mode = GROUPS;
+        p->gcu = bcu;
+        p->D = c.inflight ? c.inflight : std::max(1, std::min(3, ncu / bcu - 1));
+        p->P = 1;
+        p->split = true;
+    } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 64 && 2 * bcu > ncu) {
+        p->mode = SHARED;
+        p->rnn_kind = ASR_RNN_RECUR_MFMA;
+        const bool part = c.decode_cus != -1 && (c.decode_cus > 0 || u <= 4);
+        p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : ncu / 2 / 8 * 8) : 0;
+        p->D = c.inflight ? c.inflight : (part ? std::max(2, (3 + u - 1) / u) : std::max(1, (3 + u - 1) / u));
+        p->P = c.prod_streams ? c.prod_streams : (part ? 3 : 1);
+    } else {
+        p->mode = GROUPS2;
+        p->gcu = std::min(bcu, ncu / 4);
+        p->D = c.inflight ? c.inflight : std::max(1, std::min(2, ncu / std::max(1, p->gcu) - 1));
+        p->P = c.prod_streams ? c.prod_streams : (c.H > 256 ? 2 : 1);
+        if (p->D == 1) p->gcu = 0;
+    }
+    if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
+    p->nbuf = p->D + p->P;
+    if (p->nbuf < 2) p->nbuf = 2;
+    // streams
+    auto mk = [&](hipStream_t* s, int lo, int hi) { return rc ? rc : (rc = cu_stream(s, ncu, lo, hi)); };
+    p->s_dec.assign(p->D, nullptr);
+    p->s_prod.assign(p->P, nullptr);
+    if (p->mode == SHARED) {
+        for (int d = 0; d < p->D; d++) mk(&p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
+        for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->dcus, ncu);
+    } else {
+        for (int d = 0; d < p->D; d++)
+            mk(&p->s_dec[d], p->gcu ? d * p->gcu : 0, p->gcu ? (d + 1) * p->gcu : ncu);
+        for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->gcu ? p->D * p->gcu : 0, ncu);
+        if (p->split) mk(&p->s_gemm, 0, ncu);   // the GEMMs on every CU
+    }
+    // buffers, decoders, events
+    const size_t nh = (size_t)c.T * c.B * c.H, ne = (size_t)c.T * c.B * c.V;
+    for (int k = 0; k < p->nbuf && !rc; k++) {
+        float *hb = nullptr, *eb = nullptr;
+        if (hipMalloc(&hb, nh * sizeof(float)) != hipSuccess) rc = ASR_ERR_OOM;
+        p->hid.push_back(hb);
+        if (!rc && hipMalloc(&eb, ne * sizeof(float)) != hipSuccess) rc = ASR_ERR_OOM;
+        p->emis.push_back(eb);
+        asr_ctc_t* h = nullptr;
+        if (!rc) rc = asr_ctc_create(nullptr, c.V, c.beam, c.blank, 0, &h);
+        p->dec.push_back(h);
+        if (!rc && p->mode == SHARED && p->D > 1) rc = asr_ctc_set_concurrency(h, p->D);
+        for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec}) {
+            hipEvent_t e = nullptr;
+            if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;
+            v->push_back(e);
+        }
+    }
+    if (rc) {
+        release(p);
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return ASR_OK;
+}
+
+int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
+    if (!p || !x) return ASR_ERR_ARG;
+    const long i = p->submitted;
+    // buffer i % nbuf is reused: its previous batch's results must be fetched first
+    while (i - p->collected >= p->nbuf) {
+        Result r;
+        int rc = fetch(p, r);
+        if (rc) return rc;
+        p->stash.push_back(std::move(r));
+    }
+    int rc;
+    if (p->split) {
+        rc = produce_head(p, i, x);
+        p->submitted = i + 1;
+        if (!rc) rc = flush_tail(p);   // the previous batch: emission GEMM after this batch's input GEMM
+        p->pending_tail = i;
+    } else {
+        rc = produce_full(p, i, x);
+        p->submitted = i + 1;
+        if (!rc) rc = enqueue_decode(p, i);
+    }
+    return rc;
+}
+
+int asr_pipeline_collect(asr_pipeline_t* p, int32_t* labels, int max_len, int32_t* lengths, double* logp,
+                         float* decode_ms) {
+    if (!p || (!labels && max_len > 0)) return ASR_ERR_ARG;
+    Result r;
+    if (!p->stash.empty()) {
+        r = std::move(p->stash.front());
+        p->stash.pop_front();
+    } else {
+        int rc = fetch(p, r);
+        if (rc) return rc;
+    }
+    const auto& c = p->cfg;
+    for (int b = 0; b < c.B; b++) {
+        const int len = r.len[b];
+        if (lengths) lengths[b] = len;
+        if (logp) logp[b] = r.lp[b];
+        if (labels) {
+            const int n = std::min(len, max_len);
+            std::memcpy(labels + (size_t)b * max_len, r.lab.data() + (size_t)b * c.T, sizeof(int32_t) * n);
+        }
+    }
+    if (decode_ms) *decode_ms = r.ms;
+    return r.rc;
+}
+
+int asr_pipeline_pending(asr_pipeline_t* p, int* n) {
+    if (!p || !n) return ASR_ERR_ARG;
+    *n = (int)(p->submitted - p->collected);
+    return ASR_OK;
+}
+
+int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod_streams, int* decode_cus,
+                          int* decode_waves) {
+    if (!p) return ASR_ERR_ARG;
+    if (decode_waves) {   // the schedule of the last decode (before any: that of this batch size)
+        const asr_ctc_t* last = p->dec[p->decoded > 0 ? (p->decoded - 1) % p->nbuf : 0];
+        int w = 0;
+        const int rc = asr_ctc_get_config(const_cast<asr_ctc_t*>(last), nullptr, &w, nullptr);
+        if (rc) return rc;
+        *decode_waves = w;
+    }
+    if (mode) *mode = p->mode;
+    if (inflight) *inflight = p->D;
+    if (prod_streams) *prod_streams = p->P;
+    if (decode_cus) *decode_cus = p->mode == SHARED ? (p->dcus ? p->dcus : p->ncu) : (p->gcu ? p->gcu : p->ncu);
+    return ASR_OK;
+}
+
+int asr_pipeline_destroy(asr_pipeline_t* p) {
+    if (!p) return ASR_OK;
+    release(p);
+    delete p;
+    return ASR_OK;
+}
+
+}  // extern "C"

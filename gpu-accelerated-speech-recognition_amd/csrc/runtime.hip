@@ -17,6 +17,8 @@ namespace {
 thread_local std::string g_last_error;
 }
 
+thread_local int asr_internal_rnn_kind = -1;
+
 void asr_internal_set_error(const char* what, const char* msg, const char* file, int line) {
     char buf[512];
     snprintf(buf, sizeof buf, "%s: %s (%s:%d)", what, msg, file, line);
@@ -186,7 +188,8 @@ static std::atomic<int> g_rnn_recur_kind{ASR_RNN_RECUR_AUTO};   // asr_rnn_set_r
 static bool rnn_use_mfma(int B, int H) {
     if ((H & 15) != 0) return false;
     if (const char* f = getenv("ASR_RNN_MFMA")) return atoi(f) != 0;
-    const int kind = g_rnn_recur_kind.load(std::memory_order_relaxed);
+    const int kind = asr_internal_rnn_kind >= 0 ? asr_internal_rnn_kind
+                                                : g_rnn_recur_kind.load(std::memory_order_relaxed);
     if (kind != ASR_RNN_RECUR_AUTO) return kind == ASR_RNN_RECUR_MFMA;
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

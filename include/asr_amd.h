@@ -255,6 +255,48 @@ int asr_ctc_set_waves(asr_ctc_t* h, int waves);
 int asr_ctc_set_concurrency(asr_ctc_t* h, int n);
 int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes);
 
+/* ---- throughput pipeline (no reference counterpart: the reference runs one
+ *      batch at a time with host syncs between calls, main.cpp:40-72,
+ *      RNN.cu:9-30, CTCBeamSearch.cu:262-312) ---------------------------------
+ * RNN (one layer, h0 = 0) -> Linear + log_softmax -> CTC beam search over a
+ * stream of equal-shape batches.  The library owns the streams, buffers and
+ * decoder handles and overlaps the production of later batches with the
+ * decodes of earlier ones, placing the kernels on the CUs for the shape
+ * (DESIGN.md §7c).  Weights are caller-owned device arrays in the layouts of
+ * asr_rnn_fwd / asr_linear_fwd and must outlive the pipeline. */
+typedef struct asr_pipeline asr_pipeline_t;
+typedef struct asr_pipeline_config {
+    int T, B;            /* frames and utterances per batch */
+    int in, H, V;        /* feature, hidden and vocabulary (incl. blank) sizes */
+    int beam, blank;     /* decoder beam width and blank id (CPU semantics) */
+    int inflight;        /* decodes in flight (0 = automatic) */
+    int prod_streams;    /* production streams (0 = automatic) */
+    int decode_cus;      /* chip-filling batches: CUs given to decoding (0 = automatic,
+                            -1 = every stream on every CU) */
+} asr_pipeline_config;
+int asr_pipeline_create(const asr_pipeline_config* cfg, const float* d_W_ih, const float* d_W_hh,
+                        const float* d_b_ih, const float* d_b_hh, const float* d_W_out,
+                        const float* d_b_out, asr_pipeline_t** out);
+/* Enqueue one batch: features d_x [T*B, in] (time-major, device; read by the
+ * batch's production, so it must stay unmodified until the batch is
+ * collected).  Returns once the work is queued; when the caller is as many
+ * batches behind as the pipeline has buffers, the oldest batch's results are
+ * fetched internally first (asr_pipeline_collect still returns them). */
+int asr_pipeline_submit(asr_pipeline_t* p, const float* d_x);
+/* Results of the oldest uncollected batch, in submission order (blocks):
+ * h_labels[B][max_len], h_lengths[B], h_logp[B] as asr_ctc_get_best, and the
+ * batch's beam-search kernel time (ms; may be NULL). */
+int asr_pipeline_collect(asr_pipeline_t* p, int32_t* h_labels, int max_len, int32_t* h_lengths,
+                         double* h_logp, float* decode_ms);
+int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
+/* The schedule chosen: mode (0 CU groups for small batches, 1 chip-filling
+ * batches, 2 CU groups for H > 256), decodes in flight, production streams,
+ * CUs per decode group / decode partition, and the decoder's waves per
+ * utterance in the last decode.  Any pointer may be NULL. */
+int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod_streams, int* decode_cus,
+                          int* decode_waves);
+int asr_pipeline_destroy(asr_pipeline_t* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,96 @@
+"""Native throughput pipeline (asr_pipeline_*): RNN -> Linear + log_softmax ->
+CTC decode over a stream of batches, production and decodes overlapped on
+library-owned streams.  Every batch's results must be exactly those of the
+same batch run one call at a time (asr_rnn_fwd, asr_linear_fwd,
+asr_ctc_decode), in every schedule the library picks (CU groups for small
+batches, chip-filling batches, H > 256), for any submit / collect
+interleaving (the pipeline fetches results itself when the caller falls a
+whole buffer ring behind)."""
+import numpy as np
+import pytest
+
+from conftest import asr
+
+pytestmark = pytest.mark.gpu
+
+
+def _weights(inp, H, V, seed):
+    rng = np.random.default_rng(seed)
+    s = 1 / np.sqrt(H)
+    host = [rng.uniform(-s, s, (inp, H)), rng.uniform(-s, s, (H, H)), rng.uniform(-0.1, 0.1, (H, 1)),
+            rng.uniform(-0.1, 0.1, (H, 1)), rng.uniform(-4 * s, 4 * s, (H, V)), rng.uniform(-0.5, 0.5, (V, 1))]
+    return [asr.DeviceMatrix.from_numpy(np.asarray(a, np.float32)) for a in host]
+
+
+def _sequential(x, W, T, B, inp, H, V, beam, recur):
+    asr.rnn_set_recurrence(recur)
+    try:
+        hid, em = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, V)
+        asr.rnn_fwd(x, W[0], W[1], W[2], W[3], hid, T, B)
+        asr.linear_fwd(hid, W[4], W[5], em, asr.EPI_BIAS_LOGSOFTMAX)
+        dec = asr.CTCDecoder(V, beam, 0)
+        dec.decode_device(em.ptr, T, B, is_log=True)
+        lab, ln, lp = dec.best_arrays()
+        out = ([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy())
+        dec.close()
+        return out
+    finally:
+        asr.rnn_set_recurrence(asr.RNN_RECUR_AUTO)
+
+
+@pytest.mark.parametrize("T,B,inp,H,V,beam,mode,recur", [
+    (60, 16, 64, 64, 29, 10, "CU groups (small batches)", asr.RNN_RECUR_AUTO),
+    (40, 256, 48, 64, 29, 50, "chip-filling batches", asr.RNN_RECUR_MFMA),
+    (20, 8, 32, 384, 29, 8, "CU groups (H > 256)", asr.RNN_RECUR_AUTO),
+])
+def test_pipeline_matches_sequential(T, B, inp, H, V, beam, mode, recur):
+    W = _weights(inp, H, V, seed=T + B + H)
+    rng = np.random.default_rng(7)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(7)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert d["mode"] == mode, d
+    got = []
+
+    def take():
+        lab, ln, lp, ms = p.collect()
+        assert ms > 0.0
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+
+    # submit ahead of collecting, past the buffer ring (the pipeline then
+    # fetches the oldest results itself), then interleave
+    for x in xs[:5]:
+        p.submit(x)
+    take()
+    take()
+    for x in xs[5:]:
+        p.submit(x)
+    while p.pending():
+        take()
+    p.close()
+    assert len(got) == len(xs)
+    for i, x in enumerate(xs):
+        ref = _sequential(x, W, T, B, inp, H, V, beam, recur)
+        assert got[i][0] == ref[0], f"batch {i}: labels differ ({d})"
+        assert np.array_equal(got[i][1], ref[1]), f"batch {i}: log-probs differ ({d})"
+
+
+def test_pipeline_explicit_schedule_and_shared_cus():
+    """Explicit knobs: every stream on every CU (decode_cus = -1) and a given
+    number of decodes in flight; same results."""
+    T, B, inp, H, V, beam = 30, 300, 32, 48, 29, 20
+    W = _weights(inp, H, V, seed=3)
+    x = asr.DeviceMatrix.from_numpy(np.random.default_rng(1).uniform(-1, 1, (T * B, inp)).astype(np.float32))
+    p = asr.Pipeline(T, B, inp, H, V, beam, W, inflight=2, prod_streams=1, decode_cus=-1)
+    d = p.describe()
+    assert d["inflight"] == 2 and d["prod_streams"] == 1 and d["decode_cus"] >= 256
+    for _ in range(3):
+        p.submit(x)
+    outs = []
+    for _ in range(3):
+        lab, ln, lp, _ = p.collect()
+        outs.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    p.close()
+    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA)
+    for o in outs:
+        assert o[0] == ref[0] and np.array_equal(o[1], ref[1])
