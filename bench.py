@@ -844,7 +844,9 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
         # the pipeline's MFMA recurrence for chip-filling batches, also for
         # the 1-GPU re-decode that checks the gathered shards
         asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
-    lag = desc["inflight"]
+    # results of batch i are read once the pipeline's buffers hold newer work:
+    # D decoding and P producing
+    lag = desc["inflight"] + desc["prod_streams"]
     kernel_ms = []
     best = {}
 

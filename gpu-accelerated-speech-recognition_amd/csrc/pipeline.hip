@@ -228,15 +228,22 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : ncu / 2 / 8 * 8) : 0;
         p->D = c.inflight ? c.inflight : (part ? std::max(2, (3 + u - 1) / u) : std::max(1, (3 + u - 1) / u));
         p->P = c.prod_streams ? c.prod_streams : (part ? 3 : 1);
-    } else {
+    } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
-        p->gcu = std::min(bcu, ncu / 4);
-        p->D = c.inflight ? c.inflight : std::max(1, std::min(2, ncu / std::max(1, p->gcu) - 1));
+        p->gcu = bcu;
+        p->D = c.inflight ? c.inflight : std::max(1, std::min(2, ncu / bcu - 1));
         p->P = c.prod_streams ? c.prod_streams : (c.H > 256 ? 2 : 1);
         if (p->D == 1) p->gcu = 0;
+    } else {   // chip-filling batches otherwise (C3's beam 100, BL's H = 2048): one decode at a time
+        p->mode = SHARED;
+        p->dcus = c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : 0;
+        p->D = c.inflight ? c.inflight : 1;
+        p->P = c.prod_streams ? c.prod_streams : 1;
     }
     if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
-    p->nbuf = p->D + p->P;
+    // D decoding + P producing (+1: split production queues the next input
+    // projection before the previous batch's emission projection)
+    p->nbuf = p->D + p->P + (p->split ? 1 : 0);
     if (p->nbuf < 2) p->nbuf = 2;
     // streams
     auto mk = [&](hipStream_t* s, int lo, int hi) { return rc ? rc : (rc = cu_stream(s, ncu, lo, hi)); };
