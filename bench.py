@@ -850,14 +850,20 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     kernel_ms = []
     best = {}
 
+    hostlog = [] if os.environ.get("ASR_BENCH_HOSTLOG") else None   # diagnostic: host call times
+
     def take():
         lab, ln, lp, ms = pl.collect()
         kernel_ms.append(ms)
         best["arrays"] = (lab, ln, lp)
+        if hostlog is not None:
+            hostlog.append(("collect", time.perf_counter()))
 
     def run(n):
         for _ in range(n):
             pl.submit(d_x)
+            if hostlog is not None:
+                hostlog.append(("submit", time.perf_counter()))
             while pl.pending() > lag:
                 take()
         while pl.pending():
@@ -876,6 +882,10 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     asr.synchronize()
     elapsed = time.perf_counter() - t0
     gc.enable()
+    if hostlog is not None:
+        with open(os.environ["ASR_BENCH_HOSTLOG"], "w") as f:
+            for what, tt in hostlog:
+                f.write(f"{what} {1e3 * (tt - t0):.3f}\n")
     elapsed = reduce_max_over_ranks(elapsed, world)
     if world > 1:
         dist.barrier()

@@ -45,6 +45,7 @@ struct CtcArgs {
     double* best_score;     // [B]
     uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
     uint32_t* tile0;        // [B][T][WREC] first label tile per frame (wide kernel, V > 65; NULL: in-kernel)
+    int diag;               // bit 0: the wide kernel always takes its register fallback (tests; ASR_CTC_WIDE_FALLBACK=1)
 };
 
 int ctc_row_capacity(int kcap);   // compile-time slot capacity KC >= kcap (64, 128, 256)
@@ -66,10 +67,11 @@ int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
 size_t ctc_tile0_bytes(int B, int T);   // a.tile0 workspace of the wide kernel
 size_t ctc_lds_bytes_wide(int kc, int V);
 int ctc_set_max_lds_wide();
-// One wave per utterance, list-based (ctc_wave_kernel.inc): the default when supported.
+// One wave per utterance (ctc_wave_kernel.inc): batches of many utterances per CU.
 size_t ctc_lds_bytes_wave(const CtcGeom& g);
 bool ctc_wave_supported(const CtcGeom& g, int cu_mode);
 int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s);
+int ctc_occupancy_wave(const CtcGeom& g);   // one-wave workgroups per CU
 int ctc_set_max_lds_wave();
 // waves < 0: the one-wave list kernel; 1..8: the workgroup kernel with that many waves.
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);

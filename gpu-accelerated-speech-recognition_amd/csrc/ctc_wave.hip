@@ -5,11 +5,10 @@
 namespace asr {
 
 size_t ctc_lds_bytes_wave(const CtcGeom& g) {
-    const int lcap = wave_lcap(g.kcap, g.V);
     switch (ctc_row_capacity(g.kcap)) {
-    case 64: return WLds<64>::total(lcap, g.ch, g.V);
-    case 128: return WLds<128>::total(lcap, g.ch, g.V);
-    default: return WLds<256>::total(lcap, g.ch, g.V);
+    case 64: return WLds<64>::total(g.V);
+    case 128: return WLds<128>::total(g.V);
+    default: return WLds<256>::total(g.V);
     }
 }
 
@@ -27,6 +26,20 @@ int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s) {
     }
     ASR_LAUNCH_TRY();
     return ASR_OK;
+}
+
+// Utterances (one-wave workgroups) that fit on one CU at this layout's LDS
+// size (registers, LDS, wave slots: the runtime's occupancy query); 0 on failure.
+int ctc_occupancy_wave(const CtcGeom& g) {
+    const size_t lds = ctc_lds_bytes_wave(g);
+    int n = 0;
+    hipError_t e;
+    switch (ctc_row_capacity(g.kcap)) {
+    case 64: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<1>, 64, lds); break;
+    case 128: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<2>, 64, lds); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<4>, 64, lds); break;
+    }
+    return e == hipSuccess ? n : 0;
 }
 
 int ctc_set_max_lds_wave() {

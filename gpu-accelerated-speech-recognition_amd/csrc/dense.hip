@@ -502,6 +502,7 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int RNN_HMAX = 256;
 constexpr int RNN_QS = 68;   // LDS stride of one quarter (floats)
 
+template <bool PK>
 __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict__ h0,
                                                          const float* __restrict__ Whh,
                                                          const float* __restrict__ b_ih,
@@ -548,9 +549,24 @@ __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict
         pnext = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             __builtin_amdgcn_make_buffer_rsrc(base + tstride, 0, t + 1 < T ? nbytes : 0, RSRC3), voff, 0, 0));
         const float4* hq = reinterpret_cast<const float4*>(&hs[cur][q * RNN_QS]);
+        float acc = 0.f;
+        if constexpr (PK) {
+        // packed fp32 FMAs (v_pk_fma_f32: two k per lane per instruction),
+        // even / odd k in the two halves, summed at the end
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        f2v acc2 = {0.f, 0.f};
+#pragma unroll
+        for (int i4 = 0; i4 < 16; i4++) {
+            const float4 h4 = hq[i4];
+            const f2v ha = {h4.x, h4.y}, hb = {h4.z, h4.w};
+            const f2v wa = {w[4 * i4 + 0], w[4 * i4 + 1]}, wb = {w[4 * i4 + 2], w[4 * i4 + 3]};
+            acc2 = __builtin_elementwise_fma(ha, wa, acc2);
+            acc2 = __builtin_elementwise_fma(hb, wb, acc2);
+        }
+        acc = acc2.x + acc2.y;
+        } else {
         // one FMA chain: four independent chains measured slower (C2
         // recurrence 0.35 -> 0.46 ms, gpurun_out/r3m)
-        float acc = 0.f;
 #pragma unroll
         for (int i4 = 0; i4 < 16; i4++) {
             const float4 h4 = hq[i4];
@@ -558,6 +574,7 @@ __global__ __launch_bounds__(1024) void rnn_recur_kernel(const float* __restrict
             acc = fmaf(h4.y, w[4 * i4 + 1], acc);
             acc = fmaf(h4.z, w[4 * i4 + 2], acc);
             acc = fmaf(h4.w, w[4 * i4 + 3], acc);
+        }
         }
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
@@ -575,8 +592,12 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
                      float* hid, int T, int B, int H, hipStream_t s) {
     if (H > RNN_HMAX) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H * 4 > 0x7fffffe0L) return ASR_ERR_UNSUPPORTED;   // one step's rows per buffer resource
-    hipLaunchKernelGGL(rnn_recur_kernel, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid,
-                       T, B, H);
+    // packed FMAs (two k per instruction) unless ASR_RNN_PK=0 (A/B)
+    static const bool pk = [] { const char* e = getenv("ASR_RNN_PK"); return !e || atoi(e) != 0; }();
+    if (pk)
+        hipLaunchKernelGGL(rnn_recur_kernel<true>, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid, T, B, H);
+    else
+        hipLaunchKernelGGL(rnn_recur_kernel<false>, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid, T, B, H);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

@@ -427,6 +427,7 @@ struct asr_ctc {
     uint64_t* d_fin_ts = nullptr;    // [B][kcap][2] append frames of the final tails
     uint32_t* d_tile0 = nullptr;     // [B][T] first label tile per frame (wide kernel, V > 65)
     bool tile0 = true;               // precompute first tiles (ASR_CTC_TILE0=0: in-kernel, for A/B timing)
+    int diag = 0;                    // CtcArgs::diag (ASR_CTC_WIDE_FALLBACK=1: bit 0)
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
     unsigned char* h_res = nullptr;   // pinned mirror of d_res
@@ -618,6 +619,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     h->waves_override = 0;
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
     if (const char* t0 = getenv("ASR_CTC_TILE0")) h->tile0 = atoi(t0) != 0;
+    if (const char* fb = getenv("ASR_CTC_WIDE_FALLBACK")) h->diag = atoi(fb) != 0 ? 1 : 0;
     if (asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }
@@ -761,6 +763,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.nodes_ts = h->ts ? h->d_nodes_ts : nullptr;
     a.fin_ts = h->ts ? h->d_fin_ts : nullptr;
     a.tile0 = use_tile0(h) ? h->d_tile0 : nullptr;
+    a.diag = h->diag;
     // packed result layout for this (B, T)
     h->d_best_score = reinterpret_cast<double*>(h->d_res);
     h->d_best_len = reinterpret_cast<int*>(h->d_res + 8 * (size_t)B);

@@ -93,3 +93,21 @@ def test_c2_shape_best():
         assert best[b] == ref[b][0][0], f"utterance {b}"
         assert abs(lp[b] - ref[b][0][1]) <= 1e-9 * abs(ref[b][0][1])
     dec.close()
+
+
+@pytest.mark.parametrize("sigma,beam", [(3.0, 50), (0.5, 50), (1.0, 100)])
+def test_same_bits_as_workgroup_kernel(sigma, beam):
+    """The one-wave kernel keeps the workgroup kernel's arithmetic (prefix
+    scores, fold order, exact selection), so the ranked beams of a batch are
+    the same labels and the same fp64 bits — only slot order differs."""
+    T, B, V = 120, 96, 29
+    emis = oracle.synthetic_emissions(T, B, V, seed0=777 + beam, sigma=sigma)
+    got = {}
+    for w in (8, LIST):
+        dec = asr.CTCDecoder(V, beam, 0, waves=w)
+        dec.decode(emis)
+        got[w] = (dec.beams(max_hyps=dec.config()[0]), dec.best())
+        dec.close()
+    assert got[8][0] == got[LIST][0]
+    assert got[8][1][0] == got[LIST][1][0]
+    assert np.array_equal(np.asarray(got[8][1][1]), np.asarray(got[LIST][1][1]))
