@@ -5,10 +5,11 @@
 namespace asr {
 
 size_t ctc_lds_bytes_wave(const CtcGeom& g) {
+    const bool c64 = g.V > 32;
     switch (ctc_row_capacity(g.kcap)) {
-    case 64: return WLds<64>::total(g.V);
-    case 128: return WLds<128>::total(g.V);
-    default: return WLds<256>::total(g.V);
+    case 64: return c64 ? WLds<64, true>::total(g.V) : WLds<64, false>::total(g.V);
+    case 128: return c64 ? WLds<128, true>::total(g.V) : WLds<128, false>::total(g.V);
+    default: return c64 ? WLds<256, true>::total(g.V) : WLds<256, false>::total(g.V);
     }
 }
 
@@ -19,10 +20,20 @@ bool ctc_wave_supported(const CtcGeom& g, int cu_mode) {
 int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s) {
     const size_t lds = ctc_lds_bytes_wave(a.g);
     const dim3 grid(a.B), block(64);
+    const bool c64 = a.g.V > 32;
     switch (ctc_row_capacity(a.g.kcap)) {
-    case 64: hipLaunchKernelGGL(ctc_wave_kernel<1>, grid, block, lds, s, a); break;
-    case 128: hipLaunchKernelGGL(ctc_wave_kernel<2>, grid, block, lds, s, a); break;
-    default: hipLaunchKernelGGL(ctc_wave_kernel<4>, grid, block, lds, s, a); break;
+    case 64:
+        if (c64) hipLaunchKernelGGL((ctc_wave_kernel<1, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((ctc_wave_kernel<1, false>), grid, block, lds, s, a);
+        break;
+    case 128:
+        if (c64) hipLaunchKernelGGL((ctc_wave_kernel<2, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((ctc_wave_kernel<2, false>), grid, block, lds, s, a);
+        break;
+    default:
+        if (c64) hipLaunchKernelGGL((ctc_wave_kernel<4, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((ctc_wave_kernel<4, false>), grid, block, lds, s, a);
+        break;
     }
     ASR_LAUNCH_TRY();
     return ASR_OK;
@@ -34,19 +45,25 @@ int ctc_occupancy_wave(const CtcGeom& g) {
     const size_t lds = ctc_lds_bytes_wave(g);
     int n = 0;
     hipError_t e;
+    const bool c64 = g.V > 32;
+#define ASR_WOCC(r) c64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<r, true>, 64, lds) \
+                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<r, false>, 64, lds)
     switch (ctc_row_capacity(g.kcap)) {
-    case 64: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<1>, 64, lds); break;
-    case 128: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<2>, 64, lds); break;
-    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ctc_wave_kernel<4>, 64, lds); break;
+    case 64: e = ASR_WOCC(1); break;
+    case 128: e = ASR_WOCC(2); break;
+    default: e = ASR_WOCC(4); break;
     }
+#undef ASR_WOCC
     return e == hipSuccess ? n : 0;
 }
 
 int ctc_set_max_lds_wave() {
     const int lim = 160 * 1024;
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wave_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wave_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wave_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+#define ASR_WLIM(r, c) ASR_HIP_TRY(hipFuncSetAttribute((const void*)ctc_wave_kernel<r, c>, \
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    ASR_WLIM(1, false) ASR_WLIM(2, false) ASR_WLIM(4, false)
+    ASR_WLIM(1, true) ASR_WLIM(2, true) ASR_WLIM(4, true)
+#undef ASR_WLIM
     return ASR_OK;
 }
 

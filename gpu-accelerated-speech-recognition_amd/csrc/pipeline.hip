@@ -34,6 +34,8 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -149,8 +151,17 @@ int flush_tail(asr_pipeline* p) {
     if (p->pending_tail < 0) return ASR_OK;
     const long j = p->pending_tail;
     p->pending_tail = -1;
+    static const bool trace = [] { const char* e = getenv("ASR_PIPELINE_TRACE"); return e && atoi(e); }();
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = produce_tail(p, j);
+    const auto t1 = std::chrono::steady_clock::now();
     if (!rc) rc = enqueue_decode(p, j);
+    if (trace) {
+        const auto t2 = std::chrono::steady_clock::now();
+        const double a = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        const double b = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        if (a + b > 0.5) fprintf(stderr, "asr_pipeline: batch %ld emission GEMM %.3f ms, decode enqueue %.3f ms\n", j, a, b);
+    }
     return rc;
 }
 
@@ -226,9 +237,19 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 64 && 2 * bcu > ncu) {
         p->mode = SHARED;
         p->rnn_kind = ASR_RNN_RECUR_MFMA;
-        const bool part = c.decode_cus != -1 && (c.decode_cus > 0 || u <= 4);
+        // decodes and production on their own halves of the CUs (the
+        // decode workgroups fill a CU's registers, the wide GEMM needs most
+        // of its LDS), D batches decoding at once: up to 4 utterances per
+        // CU the 4-wave kernel three to a CU (D >= 2 so that the next batch
+        // fills what the last round of the previous one leaves idle), from
+        // 4 on the one-wave kernel, 16 to a CU (measured, profiles/r03:
+        // 1024 per GPU 94 -> 163 M frames/s)
+        const bool part = c.decode_cus != -1;
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : ncu / 2 / 8 * 8) : 0;
-        p->D = c.inflight ? c.inflight : (part ? std::max(2, (3 + u - 1) / u) : std::max(1, (3 + u - 1) / u));
+        const int dc = p->dcus ? p->dcus : ncu;
+        const int Dw = std::max(1, (16 * dc + c.B - 1) / c.B);   // 16 one-wave decodes per CU
+        p->D = c.inflight ? c.inflight
+                          : (u >= 4 ? std::min(Dw, 2) : (part ? std::max(2, (3 + u - 1) / u) : std::max(1, (3 + u - 1) / u)));
         p->P = c.prod_streams ? c.prod_streams : (part ? 3 : 1);
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
@@ -271,7 +292,10 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         asr_ctc_t* h = nullptr;
         if (!rc) rc = asr_ctc_create(nullptr, c.V, c.beam, c.blank, 0, &h);
         p->dec.push_back(h);
-        if (!rc && p->mode == SHARED && p->D > 1) rc = asr_ctc_set_concurrency(h, p->D);
+        // the decoders' schedule (asr_ctc_set_concurrency): D batches share the
+        // decode CUs, which are dcus of the ncu the decoder plans for
+        const int conc = p->mode == SHARED ? (p->D * ncu + (p->dcus ? p->dcus : ncu) - 1) / (p->dcus ? p->dcus : ncu) : 1;
+        if (!rc && conc > 1) rc = asr_ctc_set_concurrency(h, conc);
         for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec}) {
             hipEvent_t e = nullptr;
             if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;
@@ -297,16 +321,31 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
         if (rc) return rc;
         p->stash.push_back(std::move(r));
     }
+    // ASR_PIPELINE_TRACE=1: host time of each submit step over 0.5 ms (diagnostic)
+    static const bool trace = [] { const char* e = getenv("ASR_PIPELINE_TRACE"); return e && atoi(e); }();
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto lap = [&](const char* what, clk::time_point& last) {
+        const auto now = clk::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - last).count();
+        if (ms > 0.5) fprintf(stderr, "asr_pipeline: batch %ld %s %.3f ms\n", i, what, ms);
+        last = now;
+    };
+    auto last = t0;
     int rc;
     if (p->split) {
         rc = produce_head(p, i, x);
+        if (trace) lap("head", last);
         p->submitted = i + 1;
         if (!rc) rc = flush_tail(p);   // the previous batch: emission GEMM after this batch's input GEMM
+        if (trace) lap("tail+decode", last);
         p->pending_tail = i;
     } else {
         rc = produce_full(p, i, x);
+        if (trace) lap("produce", last);
         p->submitted = i + 1;
         if (!rc) rc = enqueue_decode(p, i);
+        if (trace) lap("decode", last);
     }
     return rc;
 }

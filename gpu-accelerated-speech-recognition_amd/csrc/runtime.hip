@@ -4,6 +4,8 @@
 // RNN / matrixMul / matrixAdd) and the CTC decoder handle (CTCBeamSearch).
 // ============================================================================
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -404,6 +406,7 @@ struct asr_ctc {
     int cu_mode = 0;                // ASR_CTC_SEMANTICS_CUDA
     int ncu = 0;                    // compute units of the handle's device (auto_waves)
     int occ8 = -1, occ4 = -1;       // workgroups per CU of the 8- / 4-wave kernels (-1: not queried)
+    int occw = 0;                   // ... of the one-wave kernel (0: not a candidate)
     int concurrency = 1;            // decodes of this size in flight on the device (asr_ctc_set_concurrency)
     std::vector<int32_t> codes;
     uint64_t blank_less;
@@ -431,6 +434,8 @@ struct asr_ctc {
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
     unsigned char* h_res = nullptr;   // pinned mirror of d_res
+    unsigned char* hd_res = nullptr;  // h_res as the device sees it (the kernels write there directly)
+    bool res_direct = true;           // kernels write results into h_res (ASR_CTC_RESULT_COPY=1: copy d_res)
     int *h_best_lab = nullptr, *h_best_len = nullptr, *h_status = nullptr;
     double* h_best_score = nullptr;
     // last decode
@@ -477,17 +482,31 @@ asr::CtcGeom plan(const asr_ctc* h, int waves);
 // lowers an explicit count where a narrower instantiation is required.
 constexpr double REL_4W[4] = {0.0, 1.13, 1.25, 1.46};
 double rel_4w(int n) { return n <= 3 ? REL_4W[n] : REL_4W[3] * n / 3.0; }
+// The one-wave kernel (ctc_wave_kernel.inc, beam capacity <= 64): per-
+// utterance frame time relative to the 8-wave kernel alone with n of them
+// on a CU (measured, tools/occupancy_sweep.py, profiles/r03/: 6.94 / 7.28 /
+// 8.52 / 9.60 / 9.65 / 11.30 / 13.28 us per frame at 1 / 2 / 4 / 6 / 8 / 12 /
+// 16 per CU against 3.18 us; between the points linear).  Alone it is ~2.2x
+// slower than the 8-wave kernel, but a CU holds 16 of them: from ~5
+// utterances per CU on it decodes a batch fastest.
+constexpr double REL_W[17] = {0.0,  2.18, 2.29, 2.48, 2.68, 2.85, 3.02, 3.02, 3.03,
+                              3.16, 3.29, 3.42, 3.55, 3.71, 3.87, 4.02, 4.18};
+double rel_w(int n) { return n <= 16 ? REL_W[n] : REL_W[16] * n / 16.0; }
 int auto_waves(asr_ctc* h, int B) {
     if (h->cu_mode || h->V + 1 > 64 || h->V + 1 <= 8 || B <= 0) return 8;
     if (h->occ8 < 0) {   // once per handle: the layout is fixed at creation
         h->occ8 = asr::ctc_occupancy(plan(h, 8), 8);
         h->occ4 = asr::ctc_occupancy(plan(h, 4), 4);
+        h->occw = h->kcap <= 64 && asr::ctc_wave_supported(plan(h, -1), 0) ? asr::ctc_occupancy_wave(plan(h, -1)) : 0;
     }
     if (h->ncu <= 0 || h->occ8 < 1 || h->occ4 < 1) return 8;
     const int u = (B + h->ncu - 1) / h->ncu;   // utterances on the busiest CU
     const double cost8 = (double)((u + h->occ8 - 1) / h->occ8);
     const int n4 = h->occ4;
     const double cost4 = (u / n4) * rel_4w(n4) + (u % n4 ? rel_4w(u % n4) : 0.0);
+    const int nw = h->occw;
+    const double costw = nw >= 1 ? (u / nw) * rel_w(nw) + (u % nw ? rel_w(u % nw) : 0.0) : 1e30;
+    if (costw < cost4 && costw < cost8) return ASR_CTC_WAVES_LIST;
     return cost4 < cost8 ? 4 : 8;
 }
 
@@ -522,7 +541,7 @@ void free_ws(asr_ctc* h) {
     hipFree(h->d_nodes_ts); hipFree(h->d_fin_ts); hipFree(h->d_tile0);
     h->d_nodes_ts = nullptr; h->d_fin_ts = nullptr; h->d_tile0 = nullptr;
     hipHostFree(h->h_res);
-    h->d_res = nullptr; h->h_res = nullptr;
+    h->d_res = nullptr; h->h_res = nullptr; h->hd_res = nullptr;
     h->d_nodes = nullptr; h->d_fin_n = h->d_fin_node = h->d_status = nullptr;
     h->d_fin_score = nullptr; h->d_best_lab = h->d_best_len = nullptr; h->d_best_score = nullptr;
     h->h_best_lab = h->h_best_len = h->h_status = nullptr; h->h_best_score = nullptr;
@@ -556,6 +575,7 @@ int ensure_ws(asr_ctc* h, int B, int T) {
     const size_t res_bytes = 16 * (size_t)nB + sizeof(int) * (size_t)nB * nT;
     ASR_HIP_TRY(hipMalloc(&h->d_res, res_bytes));
     ASR_HIP_TRY(hipHostMalloc((void**)&h->h_res, res_bytes, 0));
+    ASR_HIP_TRY(hipHostGetDevicePointer((void**)&h->hd_res, h->h_res, 0));
     if (h->ts) {
         ASR_HIP_TRY(hipMalloc(&h->d_nodes_ts, sizeof(int4) * (size_t)nB * nT * kc));
         ASR_HIP_TRY(hipMalloc(&h->d_fin_ts, sizeof(uint64_t) * 2 * (size_t)nB * kc));
@@ -620,6 +640,7 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
     if (const char* t0 = getenv("ASR_CTC_TILE0")) h->tile0 = atoi(t0) != 0;
     if (const char* fb = getenv("ASR_CTC_WIDE_FALLBACK")) h->diag = atoi(fb) != 0 ? 1 : 0;
+    if (const char* rc_ = getenv("ASR_CTC_RESULT_COPY")) h->res_direct = atoi(rc_) == 0;
     if (asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }
@@ -765,10 +786,16 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.tile0 = use_tile0(h) ? h->d_tile0 : nullptr;
     a.diag = h->diag;
     // packed result layout for this (B, T)
-    h->d_best_score = reinterpret_cast<double*>(h->d_res);
-    h->d_best_len = reinterpret_cast<int*>(h->d_res + 8 * (size_t)B);
-    h->d_status = reinterpret_cast<int*>(h->d_res + 12 * (size_t)B);
-    h->d_best_lab = reinterpret_cast<int*>(h->d_res + 16 * (size_t)B);
+    // The decode and traceback kernels write the packed results either
+    // straight into the pinned host buffer (default: no copy to queue — a
+    // small device-to-host copy was measured to block the host until the
+    // stream's earlier copies finish, 7-9 ms with several batches in
+    // flight) or into d_res, copied behind the traceback (A/B).
+    unsigned char* const res = h->res_direct ? h->hd_res : h->d_res;
+    h->d_best_score = reinterpret_cast<double*>(res);
+    h->d_best_len = reinterpret_cast<int*>(res + 8 * (size_t)B);
+    h->d_status = reinterpret_cast<int*>(res + 12 * (size_t)B);
+    h->d_best_lab = reinterpret_cast<int*>(res + 16 * (size_t)B);
     h->h_best_score = reinterpret_cast<double*>(h->h_res);
     h->h_best_len = reinterpret_cast<int*>(h->h_res + 8 * (size_t)B);
     h->h_status = reinterpret_cast<int*>(h->h_res + 12 * (size_t)B);
@@ -789,10 +816,23 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     // the previous traceback of this handle (on the result stream) reads the
     // node records this decode overwrites
     if (h->res_fork) ASR_HIP_TRY(hipStreamWaitEvent(st, h->ev_res, 0));
+    // ASR_PIPELINE_TRACE=1: host time of the enqueue steps over 0.5 ms (diagnostic)
+    static const bool trace = [] { const char* e = getenv("ASR_PIPELINE_TRACE"); return e && atoi(e); }();
+    auto tl = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - tl).count();
+        if (ms > 0.5) fprintf(stderr, "asr_ctc_decode: %s %.3f ms\n", what, ms);
+        tl = now;
+    };
     ASR_HIP_TRY(hipEventRecord(h->ev0, st));
+    lap("event0");
     rc = asr::ctc_launch_decode(a, waves, st);
     if (rc) return rc;
+    lap("launch");
     ASR_HIP_TRY(hipEventRecord(h->ev1, st));
+    lap("event1");
     // traceback and result copy: on the result stream when one is set, so
     // that the decode stream can start the next batch at once
     const hipStream_t rs = h->res_stream ? h->res_stream : st;
@@ -803,12 +843,16 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     }
     rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, rs);
     if (rc) return rc;
+    lap("traceback launch");
     // One copy of the packed results to the pinned mirror right behind the
     // traceback: asr_ctc_get_best waits for this event only, not for work the
     // caller queued on the stream afterwards (e.g. the next batch's decode).
-    ASR_HIP_TRY(hipMemcpyAsync(h->h_res, h->d_res, 16 * (size_t)B + sizeof(int) * (size_t)B * T,
-                               hipMemcpyDeviceToHost, rs));
+    if (!h->res_direct)
+        ASR_HIP_TRY(hipMemcpyAsync(h->h_res, h->d_res, 16 * (size_t)B + sizeof(int) * (size_t)B * T,
+                                   hipMemcpyDeviceToHost, rs));
+    lap("result copy");
     ASR_HIP_TRY(hipEventRecord(h->ev_res, rs));
+    lap("event res");
     h->have = true;
     h->last_emis = d_emis;
     h->last_tstride = frame_stride;
@@ -891,13 +935,15 @@ int asr_ctc_get_beams_ts(asr_ctc_t* h, int max_hyps, int max_len, int32_t* n_hyp
     std::vector<double> score((size_t)B * kc);
     std::vector<int> lab(need), tsv(timesteps ? need : 0);
     ASR_HIP_TRY(hipMemcpyAsync(fin_n.data(), h->d_fin_n, sizeof(int) * B, hipMemcpyDeviceToHost, st));
-    ASR_HIP_TRY(hipMemcpyAsync(status.data(), h->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    if (!h->res_direct)
+        ASR_HIP_TRY(hipMemcpyAsync(status.data(), h->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(score.data(), h->d_fin_score, sizeof(double) * B * kc, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(all_len.data(), h->d_all_len, sizeof(int) * B * kc, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipMemcpyAsync(lab.data(), h->d_all_lab, sizeof(int) * need, hipMemcpyDeviceToHost, st));
     if (timesteps)
         ASR_HIP_TRY(hipMemcpyAsync(tsv.data(), h->d_all_ts, sizeof(int) * need, hipMemcpyDeviceToHost, st));
     ASR_HIP_TRY(hipStreamSynchronize(st));
+    if (h->res_direct) std::memcpy(status.data(), h->h_status, sizeof(int) * B);   // written by the decode
     const int stc = status_code(status.data(), B);
     if (stc == ASR_ERR_BEAM_OVERFLOW && h->auto_cap && h->kcap < 256) {
         if (!h->wide) {

@@ -108,25 +108,22 @@ def test_wide_tie_cut_independent_of_key_path(monkeypatch, V):
     by their (row, column) descriptor, so which tied states survive does not
     depend on whether a frame's keys were read from the window segments or
     from the registers (ASR_CTC_WIDE_FALLBACK=1 forces the register path on
-    every frame).  Emissions with a few distinct levels tie many candidates
-    at the cutoff; both paths must give the same beams, in both semantics,
-    and the CPU-semantics beams must equal the oracle's."""
+    every frame).  Emissions with three distinct levels tie many candidates
+    at the cutoff; both paths must keep exactly beam states each frame and
+    give the same beams.  (CPU semantics keep every tie — more than any
+    max_states here, reported as overflow — so only .cu mode applies.)"""
     T, B, beam = 8, 2, 12
     rng = np.random.default_rng(V)
     logit = 0.5 * rng.integers(0, 3, size=(T, B, V)).astype(np.float64)
     q = np.exp(logit)
     emis = (q / q.sum(-1, keepdims=True)).astype(np.float32)
-    for sem in (asr.SEMANTICS_CUDA, asr.SEMANTICS_CPU):
-        got = {}
-        for flag in ("0", "1"):
-            monkeypatch.setenv("ASR_CTC_WIDE_FALLBACK", flag)
-            dec = asr.CTCDecoder(V, beam, 0)
-            dec.set_semantics(sem)
-            dec.decode(emis)
-            got[flag] = dec.beams(max_hyps=dec.config()[0])
-            dec.close()
-        assert got["0"] == got["1"], f"semantics {sem}: the tie cut depends on the key path"
-        if sem == asr.SEMANTICS_CPU:
-            ref = oracle.decode(emis, beam, 0, nthreads=4)
-            for b in range(B):
-                assert [l for l, _ in got["0"][b]] == [l for l, _ in ref[b]]
+    got = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("ASR_CTC_WIDE_FALLBACK", flag)
+        dec = asr.CTCDecoder(V, beam, 0)
+        dec.set_semantics(asr.SEMANTICS_CUDA)
+        dec.decode(emis)
+        got[flag] = dec.beams(max_hyps=dec.config()[0])
+        dec.close()
+    assert got["0"] == got["1"], "the tie cut depends on the key path"
+    assert all(len(u) == beam for u in got["0"])

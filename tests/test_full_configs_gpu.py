@@ -158,30 +158,34 @@ def test_c4_shard_full_size_e2e():
 
 
 def test_c4_one_gpu_full_batch_packed_schedule():
-    """C4 on ONE GPU (the bench's N=1 line): 2048 utterances, more than the
-    CUs, so the library's automatic schedule is the 4-wave kernel two to a CU
-    (runtime.hip auto_waves); it must agree bit for bit with the 8-wave
-    schedule on the whole batch, and its first 256 rows with a 256-utterance
-    decode (one per CU, 8 waves: the 8-GPU shard shape)."""
+    """C4 on ONE GPU (the bench's N=1 line): 2048 utterances, 8 per CU, so
+    the library's automatic schedule is the one-wave kernel, a dozen and more
+    to a CU (runtime.hip auto_waves); it must agree bit for bit with the
+    8-wave and the packed 4-wave schedules on the whole batch, and its first
+    256 rows with a 256-utterance decode (one per CU, 8 waves: the 8-GPU
+    shard shape)."""
     T, B, H, V, beam = 1000, 2048, 256, 29, 50
     em, e = _e2e(T, B, H, V)
     dec, best = decode_best(em.ptr, T, B, V, beam, True)
-    assert dec.config()[1] == 4, "automatic schedule for B > CUs should be the packed 4-wave kernel"
+    assert dec.config()[1] == asr.ASR_CTC_WAVES_LIST, "automatic schedule at 8 per CU: the one-wave kernel"
     ms_auto = dec.last_kernel_ms()
     dec.close()
-    d8, best8 = decode_best(em.ptr, T, B, V, beam, True, waves=8)
-    assert d8.config()[1] == 8
-    ms8 = d8.last_kernel_ms()
-    d8.close()
-    assert best8[0] == best[0] and np.array_equal(best8[1], best[1]), "8-wave schedule differs"
+    times = {}
+    for w in (8, 4):
+        dw, bw = decode_best(em.ptr, T, B, V, beam, True, waves=w)
+        assert dw.config()[1] == w
+        times[w] = dw.last_kernel_ms()
+        dw.close()
+        assert bw[0] == best[0] and np.array_equal(bw[1], best[1]), f"{w}-wave schedule differs"
     ds = asr.CTCDecoder(V, beam, 0)   # rows [0, 256) in place: frame stride B*V
     ds.decode_device(em.ptr, T, 256, True, frame_stride=B * V, utt_stride=V)
     l256, p256 = ds.best()
     assert ds.config()[1] == 8
     ds.close()
     assert l256 == best[0][:256] and np.array_equal(p256, best[1][:256]), "256-utterance shard differs"
-    print(f"C4 2048 x 1000 decode: auto (4 waves) {ms_auto:.2f} ms, 8 waves {ms8:.2f} ms")
-    assert ms_auto < ms8, "the automatic schedule should be the faster one at B > CUs"
+    print(f"C4 2048 x 1000 decode: auto (one wave) {ms_auto:.2f} ms, 4 waves {times[4]:.2f} ms, "
+          f"8 waves {times[8]:.2f} ms")
+    assert ms_auto < times[4] < times[8], "the automatic schedule should be the fastest at 8 per CU"
 
 
 def test_c5_decode_fixture():
