@@ -17,12 +17,11 @@
 //           stream over every CU, the input projection issued one batch
 //           ahead so that it overlaps the previous batch's recurrence.
 //   SHARED  batches that fill the chip (H <= 256, beam capacity <= 64; C4's
-//           shards): with <= 4 utterances per CU the decodes get half of the
-//           CUs and D >= 2 batches decode there at once (the decoder packs
-//           three 4-wave workgroups per CU: asr_ctc_set_concurrency), the
-//           production the other half on 3 streams with the MFMA
-//           recurrence; with more utterances per CU everything shares every
-//           CU, one decode at a time.
+//           shards): the decodes get half of the CUs and D batches decode
+//           there at once, 16 utterances per decode CU (the one-wave
+//           kernel's occupancy; the decoders learn the load through
+//           asr_ctc_set_concurrency), the production the other half on 3-4
+//           streams with the MFMA recurrence.
 //   GROUPS2 H > 256 (C5: 2000 per-frame recurrence launches, replayed from
 //           the library's HIP graph): D = 2 decode groups, 2 production
 //           streams on the remaining CUs.
@@ -227,7 +226,6 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     const int K = c.beam + 1;
     const int kcap = (K + std::max(8, K / 8) + 31) / 32 * 32;
     const int bcu = (c.B + 7) / 8 * 8;   // CUs at one decode workgroup per utterance
-    const int u = (c.B + ncu - 1) / ncu;  // utterances per CU
     if (c.H <= 256 && c.V + 1 <= 64 && 4 * bcu <= ncu) {
         p->mode = GROUPS;
         p->gcu = bcu;
@@ -239,18 +237,18 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->rnn_kind = ASR_RNN_RECUR_MFMA;
         // decodes and production on their own halves of the CUs (the
         // decode workgroups fill a CU's registers, the wide GEMM needs most
-        // of its LDS), D batches decoding at once: up to 4 utterances per
-        // CU the 4-wave kernel three to a CU (D >= 2 so that the next batch
-        // fills what the last round of the previous one leaves idle), from
-        // 4 on the one-wave kernel, 16 to a CU (measured, profiles/r03:
-        // 1024 per GPU 94 -> 163 M frames/s)
+        // of its LDS), D batches decoding at once so that the decode CUs
+        // hold 16 utterances each: the one-wave kernel's occupancy, where
+        // it decodes fastest (measured, profiles/r03: 2048 per GPU 107 ->
+        // 167 M frames/s, 1024 per GPU 94 -> 163 M).  Small batches need
+        // many in flight (256 per GPU: 8), and as many production streams as
+        // the recurrence's latency (T steps, whatever B) needs to keep up.
         const bool part = c.decode_cus != -1;
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : ncu / 2 / 8 * 8) : 0;
         const int dc = p->dcus ? p->dcus : ncu;
-        const int Dw = std::max(1, (16 * dc + c.B - 1) / c.B);   // 16 one-wave decodes per CU
-        p->D = c.inflight ? c.inflight
-                          : (u >= 4 ? std::min(Dw, 2) : (part ? std::max(2, (3 + u - 1) / u) : std::max(1, (3 + u - 1) / u)));
-        p->P = c.prod_streams ? c.prod_streams : (part ? 3 : 1);
+        const int Dw = std::max(1, std::min(8, (16 * dc + c.B / 2) / c.B));   // 16 decodes per CU
+        p->D = c.inflight ? c.inflight : Dw;
+        p->P = c.prod_streams ? c.prod_streams : (part ? (p->D >= 4 ? 4 : 3) : 1);
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
         p->gcu = bcu;

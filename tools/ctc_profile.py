@@ -77,17 +77,19 @@ def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
         # (relative to wave 0's frame start), averaged over frames
         crit = buf[:, 8, :].astype(np.float64).sum(axis=0) / max(1.0, buf[:, 8, 0].astype(np.float64).sum())
         out["last_wave_arrival"] = {WPOINTS[i]: round(crit[i]) for i in sorted(WPOINTS, key=lambda i: crit[i])}
-    if stamps and dec.config()[1] == 0:   # one-wave list kernel: phase clocks and counters
+    if stamps and dec.config()[1] == -1:   # one-wave kernel: phase clocks and counters
         L = asr.lib()
         buf = np.zeros((B, 16), np.uint64)
         fn = L.asr_debug_ctc_stamps
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         asr.check(fn(dec.h, buf.ctypes.data), "stamps")
         per = buf.astype(np.float64).mean(axis=0) / T
-        names = ["rows", "own cols", "ext cols", "folds", "select", "survivors", "build", "-",
-                 "M", "live labels", "refills", "fold steps", "-", "xtot", "-", "-"]
-        out["wave_per_frame"] = {names[i]: round(per[i], 2) for i in range(16) if names[i] != "-"}
-        out["cycles_total"] = round(per[:7].sum(), 1)
+        names = ["staging", "rows+own", "folds", "labels+keys", "select", "survivors", "own build",
+                 "ext build", "n:registered labels", "n:regenerated labels", "n:fallbacks", "n:extensions",
+                 "n:selection passes", "n:keys >= floor"]
+        out["wave_cycles_per_frame"] = {names[i]: round(per[i], 1) for i in range(8)}
+        out["wave_events_per_frame"] = {names[i][2:]: round(per[i], 3) for i in range(8, 14)}
+        out["cycles_total"] = round(per[:8].sum(), 1)
     elif stamps:
         L = asr.lib()
         buf = np.zeros((B, 16), np.uint64)
@@ -113,7 +115,7 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--wstamps", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--waves", default="1,2,4")
+    ap.add_argument("--waves", default="1,2,4", help="waves per utterance; -1 = the one-wave kernel")
     ap.add_argument("--cases", default="c2,c3")
     ap.add_argument("--sigmas", default="3,0.5,bench", help="synthetic emission spreads; 'bench' = bench.py's model")
     args = ap.parse_args()
@@ -123,6 +125,7 @@ def main():
     asr.set_device(0)
     ap_cases = {"c2": (500, 64, 29, 50), "c3": (1000, 256, 29, 100),
                 "s64": (300, 64, 29, 50), "s768": (300, 768, 29, 50),   # alone / three per CU
+                "s4096": (300, 4096, 29, 50),   # 16 per CU (the one-wave kernel's occupancy)
                 "c5": (2000, 32, 1000, 200)}   # C5: 32 utterances per GPU
     ap_cases = [ap_cases[c] for c in args.cases.split(",")]
     for (T, B, V, beam) in ap_cases:
