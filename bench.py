@@ -207,7 +207,7 @@ def decoder_variant(V: int, waves: int, max_states: int) -> str:
     if R > 64:
         return f"ctc_wide_kernel<{rpt},false>"
     if waves < 0:   # the one-wave kernel (ASR_CTC_WAVES_LIST)
-        return f"ctc_wave_kernel<{rpt}>"
+        return f"ctc_wave_kernel<{rpt},{'true' if V > 32 else 'false'}>"
     cls = 8 if R <= 8 else (32 if R <= 32 else 64)
     return f"ctc_beam_kernel<{waves},{cls // waves},{rpt},false>"
 

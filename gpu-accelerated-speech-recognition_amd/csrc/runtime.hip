@@ -484,13 +484,13 @@ constexpr double REL_4W[4] = {0.0, 1.13, 1.25, 1.46};
 double rel_4w(int n) { return n <= 3 ? REL_4W[n] : REL_4W[3] * n / 3.0; }
 // The one-wave kernel (ctc_wave_kernel.inc, beam capacity <= 64): per-
 // utterance frame time relative to the 8-wave kernel alone with n of them
-// on a CU (measured, tools/occupancy_sweep.py, profiles/r03/: 6.94 / 7.28 /
-// 8.52 / 9.60 / 9.65 / 11.30 / 13.28 us per frame at 1 / 2 / 4 / 6 / 8 / 12 /
-// 16 per CU against 3.18 us; between the points linear).  Alone it is ~2.2x
-// slower than the 8-wave kernel, but a CU holds 16 of them: from ~5
+// on a CU (measured, tools/occupancy_sweep.py, profiles/r03/: 5.86 / 6.00 /
+// 6.24 / 7.09 / 8.09 / 8.12 / 9.35 / 11.13 us per frame at 1 / 2 / 3 / 4 / 6 /
+// 8 / 12 / 16 per CU against 3.18 us; between the points linear).  Alone it
+// is ~1.8x slower than the 8-wave kernel, but a CU holds 16 of them: from 4
 // utterances per CU on it decodes a batch fastest.
-constexpr double REL_W[17] = {0.0,  2.18, 2.29, 2.48, 2.68, 2.85, 3.02, 3.02, 3.03,
-                              3.16, 3.29, 3.42, 3.55, 3.71, 3.87, 4.02, 4.18};
+constexpr double REL_W[17] = {0.0,  1.84, 1.89, 1.96, 2.23, 2.39, 2.54, 2.55, 2.55,
+                              2.65, 2.74, 2.84, 2.94, 3.08, 3.22, 3.36, 3.50};
 double rel_w(int n) { return n <= 16 ? REL_W[n] : REL_W[16] * n / 16.0; }
 int auto_waves(asr_ctc* h, int B) {
     if (h->cu_mode || h->V + 1 > 64 || h->V + 1 <= 8 || B <= 0) return 8;

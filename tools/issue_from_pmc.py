@@ -10,8 +10,9 @@ SQ_ACTIVE_INST_ANY.  Units (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_INST_* count quad-cycles (x4 = shader cycles); WAIT_ANY +
 WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES.
 
-Derived, per launch (one workgroup of NW waves per utterance, one workgroup
-per CU at the bench's batch, every wave alive for the whole kernel):
+Derived, per launch (every wave alive for the whole kernel; --cus: the CUs
+the decode ran on, default one workgroup per CU = B CUs — the one-wave
+kernel packs 16 utterances per CU, so pass the decode partition):
   kernel_cycles  = 4 * WAVE_CYCLES / WAVES   (a wave's lifetime in cycles)
   per wave-frame = INSTS_x / WAVES / T
   active_frac    = ACTIVE_INST_ANY / WAVE_CYCLES  (cycles a wave issues)
@@ -42,6 +43,7 @@ def main():
     ap.add_argument("--workload", default="C2")
     ap.add_argument("--source", default="")
     ap.add_argument("--round", default="r03")
+    ap.add_argument("--cus", type=int, default=0, help="CUs the decode ran on (default: B)")
     args = ap.parse_args()
     per = {}   # dispatch -> counter -> value
     variants = set()
@@ -53,6 +55,7 @@ def main():
     if len(variants) != 1:
         raise SystemExit(f"expected one variant of {args.kernel}, found {sorted(variants)}")
     variant = variants.pop()
+    cus = args.cus or args.B
     if not per:
         raise SystemExit(f"no {args.kernel} dispatches in {args.csv}")
     keys = sorted({k for d in per.values() for k in d})
@@ -72,9 +75,10 @@ def main():
         "active_frac": round(avg["SQ_ACTIVE_INST_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
         "wait_frac": round(avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
         "stall_frac": round(avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
-        "salu_util": round(avg["SQ_INSTS_SALU"] / args.B / cyc, 4),
-        "valu_util": round(2.0 * avg["SQ_INSTS_VALU"] / (4 * args.B) / cyc, 4),
-        "lds_util": round(2.0 * avg["SQ_INSTS_LDS"] / args.B / cyc, 4),
+        "cus": cus,
+        "salu_util": round(avg["SQ_INSTS_SALU"] / cus / cyc, 4),
+        "valu_util": round(2.0 * avg["SQ_INSTS_VALU"] / (4 * cus) / cyc, 4),
+        "lds_util": round(2.0 * avg["SQ_INSTS_LDS"] / cus / cyc, 4),
     }
     out = {"T": args.T, "B": args.B,
            "counters_avg_per_launch": {k: round(v) for k, v in avg.items()},
