@@ -759,9 +759,9 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
             for (f, h, l) in records:
                 nb = len(h)
                 xg = DM(make_features(T, nb, In, f))
-                hid_g, em_g = asr.DeviceMatrix(T * nb, H), asr.DeviceMatrix(T * nb, V)
-                asr.rnn_fwd(xg, d_wih, d_whh, d_bih, d_bhh, hid_g, T, nb)
-                asr.linear_fwd(hid_g, d_wout, d_bout, em_g, asr.EPI_BIAS_LOGSOFTMAX)
+                em_g = asr.DeviceMatrix(T * nb, V)
+                asr.model_emissions(xg, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, nb, em_g,
+                                    bool((sched or {}).get("fused_emission")))
                 dg = asr.CTCDecoder(V, beam, 0, waves=args.waves)
                 dg.decode_device(em_g.ptr, T, nb, is_log=True)
                 lab1, lp1 = dg.best()
@@ -802,7 +802,8 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
 
     mfma = None
     if rank == 0 and world == 1 and not args.decode_only:
-        mfma = measure_gemms(asr, d_x, d_wih, d_hid0, d_wout, d_bout, d_emis0, T, B, In, H, V)
+        mfma = measure_gemms(asr, d_x, d_wih, d_hid0, d_wout, d_bout, d_emis0, T, B, In, H, V,
+                             fused=(d_whh, d_bih, d_bhh) if (sched or {}).get("fused_emission") else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -898,13 +899,14 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     # buffers for the GEMM timing and one batch's real emissions for the CPU baseline
     hid0, em0 = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, V)
     em_real = asr.DeviceMatrix(T * B, V)
+    fused = desc["fused_emission"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        asr.rnn_fwd(d_x, d_wih, d_whh, d_bih, d_bhh, hid0, T, B)
-        asr.linear_fwd(hid0, d_wout, d_bout, em_real, asr.EPI_BIAS_LOGSOFTMAX)
+        asr.model_emissions(d_x, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, B, em_real, fused, work=hid0)
     finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
            (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_real,
            {"inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
-            "decode_cus": desc["decode_cus"],
+            "decode_cus": desc["decode_cus"], "fused_emission": fused,
+            "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
                         f"library-owned streams, buffers and decoder schedule"})
@@ -1053,18 +1055,28 @@ def destroy_raw_streams():
         hip.hipStreamDestroy(ctypes.c_void_p(st))
 
 
-def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V, reps=10):
-    """MFMA utilisation of the two GEMMs of a step, timed live with HIP events
-    on torch's current stream after the timed region: the hoisted input
-    projection x.W_ih ([T*B, In] x [In, H]) and the emission projection with
-    its fused bias + log_softmax ([T*B, H] x [H, V])."""
+def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V, reps=10, fused=None):
+    """MFMA utilisation of the dense stages of a step, timed live with HIP
+    events on torch's current stream after the timed region: the hoisted input
+    projection x.W_ih ([T*B, In] x [In, H]), the emission projection with its
+    fused bias + log_softmax ([T*B, H] x [H, V]), and — when the pipeline fuses
+    it (fused = (W_hh, b_ih, b_hh)) — the recurrence + emission kernel
+    (asr_rnn_emit_fwd, T steps of [B x H] . [H x (H + V)]; one launch on the
+    whole chip, so its utilisation is that of ceil(B / 16) CUs' worth of work
+    spread over the launch time)."""
     st = torch.cuda.current_stream()
     out = {}
-    for name, fn, flops in (
-            ("input_gemm", lambda: asr.linear_fwd(d_x, d_wih, None, d_hid, asr.EPI_NONE, st.cuda_stream),
-             2.0 * T * B * In * H),
-            ("emission_gemm", lambda: asr.linear_fwd(d_hid, d_wout, d_bout, d_emis, asr.EPI_BIAS_LOGSOFTMAX,
-                                                     st.cuda_stream), 2.0 * T * B * H * V)):
+    stages = [
+        ("input_gemm", lambda: asr.linear_fwd(d_x, d_wih, None, d_hid, asr.EPI_NONE, st.cuda_stream),
+         2.0 * T * B * In * H),
+        ("emission_gemm", lambda: asr.linear_fwd(d_hid, d_wout, d_bout, d_emis, asr.EPI_BIAS_LOGSOFTMAX,
+                                                 st.cuda_stream), 2.0 * T * B * H * V)]
+    if fused is not None:
+        whh, bih, bhh = fused
+        stages.append(("recurrence_emission", lambda: asr.rnn_emit_fwd(whh, bih, bhh, d_wout, d_bout, d_hid,
+                                                                       d_emis, T, B, stream=st.cuda_stream),
+                       2.0 * T * B * H * (H + V)))
+    for name, fn, flops in stages:
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
@@ -1078,6 +1090,11 @@ def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V
         out[name] = {"us": round(us, 2), "tflops": round(tf, 2),
                      "mfma_util": round(tf / FP32_MFMA_PEAK_TF, 4),
                      "hbm_gbs": round(hbm / (us * 1e-6) / 1e9, 1)}
+        if name == "recurrence_emission":   # per busy CU: one 16-utterance workgroup per CU
+            busy = min(-(-B // 16), torch.cuda.get_device_properties(st.device).multi_processor_count)
+            ncu = torch.cuda.get_device_properties(st.device).multi_processor_count
+            out[name]["mfma_util_busy_cus"] = round(tf / (FP32_MFMA_PEAK_TF * busy / ncu), 4)
+            out[name]["busy_cus"] = busy
     return out
 
 
@@ -1103,9 +1120,9 @@ def cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V
         # C4 shape (T=1000, beam=50): emissions from the same model at T=1000
         T4 = 1000
         x4 = asr.DeviceMatrix.from_numpy(make_features(T4, S, In, 0))
-        h4, e4 = asr.DeviceMatrix(T4 * S, H), asr.DeviceMatrix(T4 * S, V)
-        asr.rnn_fwd(x4, d_wih, d_whh, d_bih, d_bhh, h4, T4, S)
-        asr.linear_fwd(h4, d_wout, d_bout, e4, asr.EPI_BIAS_LOGSOFTMAX)
+        e4 = asr.DeviceMatrix(T4 * S, V)
+        asr.model_emissions(x4, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T4, S, e4,
+                            fused=H % 16 == 0 and V <= 32)
         em4 = e4.toCpu().reshape(T4, S, V)
         s4 = oracle.time_decode(em4, beam, 0, is_log=True, nthreads=threads)
         out["c4_shape"] = {"value": round(S * T4 / s4, 1), "unit": "frames/s", "cores": threads,

@@ -49,14 +49,14 @@ EXPORTS = [
     "asr_host_free", "asr_memcpy_h2d", "asr_memcpy_d2h", "asr_memcpy_d2d", "asr_memset",
     "asr_stream_create", "asr_stream_destroy", "asr_stream_sync", "asr_device_sync",
     "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
-    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_recur_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
+    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_recur_fwd", "asr_rnn_emit_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
     "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
     "asr_ctc_set_concurrency", "asr_rnn_set_recurrence",
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
-    "asr_pipeline_describe", "asr_pipeline_destroy",
+    "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_destroy",
 ]
 
 
@@ -110,6 +110,7 @@ def lib() -> ctypes.CDLL:
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_set_recurrence": [_i],
+        "asr_rnn_emit_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_pipeline_create": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)],
         "asr_pipeline_submit": [_vp, _vp],
         "asr_pipeline_collect": [_vp, _vp, _i, _vp, _vp, _vp],
@@ -117,6 +118,7 @@ def lib() -> ctypes.CDLL:
         "asr_pipeline_describe": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
                                   ctypes.POINTER(_i)],
         "asr_pipeline_destroy": [_vp],
+        "asr_pipeline_get_production": [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_longlong)],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -254,6 +256,21 @@ def rnn_recur_fwd(W_hh: DeviceMatrix, b_ih: DeviceMatrix, b_hh: DeviceMatrix, hi
     check(lib().asr_rnn_recur_fwd(h0.ptr if h0 else None, W_hh.ptr, b_ih.ptr, b_hh.ptr, hid.ptr,
                                   T, B, H, stream), "asr_rnn_recur_fwd")
     return hid
+
+
+def rnn_emit_fwd(W_hh: DeviceMatrix, b_ih: DeviceMatrix, b_hh: DeviceMatrix, W_out: DeviceMatrix,
+                 b_out: DeviceMatrix, P: DeviceMatrix, emis: DeviceMatrix, T: int, B: int,
+                 h0: Optional[DeviceMatrix] = None, hid: Optional[DeviceMatrix] = None,
+                 stream: int = 0) -> DeviceMatrix:
+    """Recurrence + emission projection + log_softmax in one kernel
+    (asr_rnn_emit_fwd): P holds x.W_ih (unchanged), emis [T*B, V] receives the
+    log-probabilities, hid (optional) the hidden states."""
+    H, V = W_hh.cols, W_out.cols
+    assert P.rows == T * B and P.cols == H and emis.rows == T * B and emis.cols == V
+    check(lib().asr_rnn_emit_fwd(h0.ptr if h0 else None, W_hh.ptr, b_ih.ptr, b_hh.ptr, W_out.ptr,
+                                 b_out.ptr, P.ptr, hid.ptr if hid else None, emis.ptr, T, B, H, V,
+                                 stream), "asr_rnn_emit_fwd")
+    return emis
 
 
 def rnn_bidir_fwd(x: DeviceMatrix, params: Sequence[Tuple[DeviceMatrix, ...]], out: DeviceMatrix,
@@ -489,6 +506,24 @@ class PipelineConfig(ctypes.Structure):
 PIPELINE_MODES = {0: "CU groups (small batches)", 1: "chip-filling batches", 2: "CU groups (H > 256)"}
 
 
+def model_emissions(x: "DeviceMatrix", weights, T: int, B: int, emis: "DeviceMatrix", fused: bool,
+                    work: Optional["DeviceMatrix"] = None, stream: int = 0) -> "DeviceMatrix":
+    """One batch's emissions the way a Pipeline produces them
+    (asr_pipeline_get_production): fused — input projection GEMM, then the
+    recurrence with the emission layer fused (asr_rnn_emit_fwd); otherwise
+    asr_rnn_fwd then asr_linear_fwd(..., log_softmax).  weights = (W_ih, W_hh,
+    b_ih, b_hh, W_out, b_out); work [T*B, H] is scratch (allocated if None)."""
+    W_ih, W_hh, b_ih, b_hh, W_out, b_out = weights
+    work = work if work is not None else DeviceMatrix(T * B, W_hh.cols)
+    if fused:
+        linear_fwd(x, W_ih, None, work, EPI_NONE, stream)
+        rnn_emit_fwd(W_hh, b_ih, b_hh, W_out, b_out, work, emis, T, B, stream=stream)
+    else:
+        rnn_fwd(x, W_ih, W_hh, b_ih, b_hh, work, T, B, stream=stream)
+        linear_fwd(work, W_out, b_out, emis, EPI_BIAS_LOGSOFTMAX, stream)
+    return emis
+
+
 class Pipeline:
     """asr_pipeline_*: RNN -> Linear + log_softmax -> CTC decode over a stream of
     equal-shape batches, the library overlapping production and decodes on its
@@ -513,8 +548,12 @@ class Pipeline:
         m, d, p, c, w = _i(), _i(), _i(), _i(), _i()
         check(lib().asr_pipeline_describe(self.h, ctypes.byref(m), ctypes.byref(d), ctypes.byref(p),
                                           ctypes.byref(c), ctypes.byref(w)), "asr_pipeline_describe")
+        fz, gr = _i(), ctypes.c_longlong()
+        check(lib().asr_pipeline_get_production(self.h, ctypes.byref(fz), ctypes.byref(gr)),
+              "asr_pipeline_get_production")
         return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
-                "decode_cus": c.value, "decode_waves": w.value}
+                "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
+                "decode_cu_gemm_rows": gr.value}
 
     def submit(self, x: "DeviceMatrix") -> None:
         check(lib().asr_pipeline_submit(self.h, x.ptr), "asr_pipeline_submit")

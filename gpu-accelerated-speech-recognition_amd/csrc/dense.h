@@ -32,6 +32,11 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 // The same recurrence on MFMA, 16 utterances per workgroup (H <= 256, H % 16 == 0).
 int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                           float* hid, int T, int B, int H, hipStream_t s);
+// The MFMA recurrence with the emission projection + log_softmax fused
+// (V <= 32): P [T][B][H] read only, hidden states to hout (NULL: not stored).
+int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
+                         const float* P, float* hout, const float* Wout, const float* bout, float* emis,
+                         int T, int B, int H, int V, hipStream_t s);
 int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
 int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
 int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);

@@ -626,17 +626,40 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 //     step and to hid.
 // Grid ceil(B / 16); block 64 * ceil(H / 32) threads.
 // ---------------------------------------------------------------------------
+//
+// EMIT (asr_rnn_emit_fwd): the emission projection + log_softmax of every
+// h_t fused into the same kernel (Linear.cu:42-49, baseline/model.py:49),
+// V <= 32, so the hidden states never go to HBM (C4: 2.1 GB written and read
+// back per batch by a separate GEMM) and the projection runs on the
+// recurrence's matrix cores: wave w contracts its own k-slice of h_t (the
+// chunks 2w, 2w + 1 it already reads as A fragments) with W_out[k-slice][32]
+// held in 16 VGPRs — 16 MFMAs beside its 128 recurrence MFMAs — and writes
+// the 16 x 32 partial to LDS; one step later the partials are summed in wave
+// order, biased and log-softmaxed per row (32 lanes per row), and stored.
+// Pipelined: step t issues h_{t-1}'s partials and finishes h_{t-2}'s row.
+// The contraction order (8 partial chains, then a fixed sum) differs from the
+// GEMM kernels' single chain: emissions agree with asr_linear_fwd to fp32
+// rounding, not bit for bit.
+// ---------------------------------------------------------------------------
 constexpr int RM_ROWS = 16;
 constexpr int RM_LD = RNN_HMAX + 4;   // LDS row stride (floats): b128 reads of a quarter-wave hit distinct banks
 constexpr int RM_NCH = RNN_HMAX / 16;  // 16-k chunks at H = 256
+constexpr int RE_VMAX = 32;           // EMIT: vocabulary columns (two 16-column tiles)
+constexpr int RE_LD = 36;             // EMIT: partial row stride (floats): a wave's C-fragment stores hit distinct banks
+constexpr int RE_PART = (RNN_HMAX / 32) * RM_ROWS * RE_LD;   // EMIT: one buffer of 8 waves' 16 x 32 partials
 
+template <bool EMIT>
 __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __restrict__ h0,
                                                              const float* __restrict__ Whh,
                                                              const float* __restrict__ b_ih,
                                                              const float* __restrict__ b_hh,
-                                                             float* __restrict__ hid, int T, int B,
-                                                             int H) {
+                                                             float* hid, float* hout,
+                                                             const float* __restrict__ Wout,
+                                                             const float* __restrict__ bout,
+                                                             float* __restrict__ emis, int T, int B,
+                                                             int H, int V) {
     __shared__ __attribute__((aligned(16))) float hs[2][RM_ROWS * RM_LD];
+    __shared__ __attribute__((aligned(16))) float ep[EMIT ? 2 : 1][EMIT ? RE_PART : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int g = lane >> 4, c = lane & 15;
     const int nch = H >> 4;                 // 16-k chunks = 16-column tiles
@@ -680,9 +703,81 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
     for (int tt = 0; tt < 2; tt++)
 #pragma unroll
         for (int j = 0; j < 4; j++) pn[tt][j] = (tv[tt] && ok[j]) ? hid[rowoff[j] + n[tt]] : 0.f;
+    // EMIT: hidden states go to hout (NULL: nowhere); otherwise in place over P
+    float* const hdst = EMIT ? hout : hid;
+    // EMIT: wo[ii][vt][e] = W_out[16 (2w + ii) + 4g + e][16 vt + c] (zero past H or V)
+    float wo[2][2][4];
+    const int nw = (nch + 1) >> 1;
+    float bo = 0.f;
+    if (EMIT) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ii++)
+#pragma unroll
+            for (int vt = 0; vt < 2; vt++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int k = 16 * (2 * w + ii) + 4 * g + e, col = 16 * vt + c;
+                    wo[ii][vt][e] = (2 * w + ii < nch && col < V) ? Wout[(long)k * V + col] : 0.f;
+                }
+        bo = (lane & 31) < V ? bout[lane & 31] : 0.f;
+    }
+    // EMIT: wave w's partial of h_s . W_out over its k-slice (chunks 2w, 2w + 1)
+    // into partial buffer s & 1 (h_s in hs[buf])
+    auto emit_partial = [&](int buf, int s) {
+        f32x4 ea[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const float* hr = &hs[buf][c * RM_LD + 4 * g];
+#pragma unroll
+        for (int ii = 0; ii < 2; ii++) {
+            const int i = 2 * w + ii;
+            if (i < nch) {
+                const float4 a = *reinterpret_cast<const float4*>(hr + 16 * i);
+#pragma unroll
+                for (int vt = 0; vt < 2; vt++) {
+                    ea[vt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wo[ii][vt][0], ea[vt], 0, 0, 0);
+                    ea[vt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wo[ii][vt][1], ea[vt], 0, 0, 0);
+                    ea[vt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wo[ii][vt][2], ea[vt], 0, 0, 0);
+                    ea[vt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wo[ii][vt][3], ea[vt], 0, 0, 0);
+                }
+            }
+        }
+        float* pp = &ep[s & 1][w * RM_ROWS * RE_LD];
+#pragma unroll
+        for (int vt = 0; vt < 2; vt++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) pp[(4 * g + j) * RE_LD + 16 * vt + c] = ea[vt][j];
+    };
+    // EMIT: emissions of frame s from partial buffer s & 1: thread (row, col)
+    // sums the waves' partials in wave order, + b_out, log_softmax over the
+    // row's 32 lanes (columns >= V are -inf), stores columns < V
+    auto emit_rows = [&](int s) {
+        const float* pp = ep[s & 1];
+        for (int idx0 = 0; idx0 < RM_ROWS * 32; idx0 += (int)blockDim.x) {
+            const int idx = idx0 + tid;   // whole waves in or out of range (blockDim % 64 == 0)
+            const int row = idx >> 5, col = idx & 31;
+            float v = -INFINITY;
+            if (idx < RM_ROWS * 32 && col < V) {
+                float acc = 0.f;
+                for (int q = 0; q < nw; q++) acc += pp[(q * RM_ROWS + row) * RE_LD + col];
+                v = acc + bo;
+            }
+            float mx = v;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            float se = col < V ? expf(v - mx) : 0.f;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) se += __shfl_xor(se, o);
+            const float lz = mx + logf(se);
+            if (idx < RM_ROWS * 32 && col < V && r0 + row < B)
+                emis[((long)s * B + r0 + row) * V + col] = v - lz;
+        }
+    };
     __syncthreads();
     int cur = 0;
     for (int t = 0; t < T; t++) {
+        if (EMIT) {
+            if (t >= 2) emit_rows(t - 2);
+            if (t >= 1) emit_partial(cur, t - 1);
+        }
         float p[2][4];
 #pragma unroll
         for (int tt = 0; tt < 2; tt++)
@@ -725,11 +820,17 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
             for (int j = 0; j < 4; j++) {
                 const float h = tanhf((p[tt][j] + sum[j]) + bias[tt]);
                 hn[(4 * g + j) * RM_LD + n[tt]] = h;
-                if (ok[j]) base[rowoff[j] + n[tt]] = h;
+                if (ok[j] && (!EMIT || hdst)) hdst[(long)t * tstride + rowoff[j] + n[tt]] = h;
             }
         }
         cur ^= 1;
         lds_barrier();
+    }
+    if (EMIT) {   // the last two frames' emissions
+        if (T >= 2) emit_rows(T - 2);
+        emit_partial(cur, T - 1);
+        lds_barrier();
+        emit_rows(T - 1);
     }
 }
 
@@ -737,9 +838,21 @@ int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, 
                           float* hid, int T, int B, int H, hipStream_t s) {
     if (H > RNN_HMAX || (H & 15) != 0 || B <= 0) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
-    hipLaunchKernelGGL(rnn_recur_mfma_kernel, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
+    hipLaunchKernelGGL(rnn_recur_mfma_kernel<false>, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
                        dim3(64 * ((H / 16 + 1) / 2)), 0, s,
-                       h0, Whh, b_ih, b_hh, hid, T, B, H);
+                       h0, Whh, b_ih, b_hh, hid, nullptr, nullptr, nullptr, nullptr, T, B, H, 0);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
+                         const float* P, float* hout, const float* Wout, const float* bout, float* emis,
+                         int T, int B, int H, int V, hipStream_t s) {
+    if (H > RNN_HMAX || (H & 15) != 0 || B <= 0 || V < 1 || V > RE_VMAX) return ASR_ERR_UNSUPPORTED;
+    if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
+    hipLaunchKernelGGL(rnn_recur_mfma_kernel<true>, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
+                       dim3(64 * ((H / 16 + 1) / 2)), 0, s,
+                       h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H, V);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

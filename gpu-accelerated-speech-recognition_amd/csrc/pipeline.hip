@@ -21,7 +21,9 @@
 //           there at once, 16 utterances per decode CU (the one-wave
 //           kernel's occupancy; the decoders learn the load through
 //           asr_ctc_set_concurrency), the production the other half on 3-4
-//           streams with the MFMA recurrence.
+//           streams with the MFMA recurrence — from round 3 the recurrence
+//           with the emission projection fused (asr_rnn_emit_fwd, V <= 32),
+//           part of the input projection optionally on the decode CUs.
 //   GROUPS2 H > 256 (C5: 2000 per-frame recurrence launches, replayed from
 //           the library's HIP graph): D = 2 decode groups, 2 production
 //           streams on the remaining CUs.
@@ -61,6 +63,9 @@ struct asr_pipeline {
     const float *W_out = nullptr, *b_out = nullptr;
     int ncu = 0, mode = SHARED, D = 1, P = 1, nbuf = 2, gcu = 0, dcus = 0, rnn_kind = -1;
     bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
+    bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
+    long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
+    hipStream_t s_gdec = nullptr;   // the decode CUs' share of the input projections
     std::vector<float*> hid, emis;
     std::vector<asr_ctc_t*> dec;
     std::vector<hipStream_t> s_dec, s_prod;
@@ -97,6 +102,40 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     asr_internal_rnn_kind = -1;
     if (!rc) rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
                                  ASR_EPI_BIAS_LOGSOFTMAX, sp);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
+    return ASR_OK;
+}
+
+// Fused production of batch i into buffer k (chip-filling batches, H <= 256,
+// V <= 32): the input projection P = x.W_ih into hid[k] — its first grows rows
+// on the decode CUs (s_gdec, which runs them whenever the decodes leave those
+// CUs free, so the decode and production halves of the chip carry equal
+// work), the rest on the production stream — then the recurrence with the
+// emission projection + log_softmax fused (asr_rnn_emit_fwd: the hidden
+// states never go to HBM).  Rows are independent, so the split never changes
+// a bit (the wide and tiled GEMM kernels accumulate in the same k order).
+int produce_fused(asr_pipeline* p, long i, const float* x) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    hipStream_t sp = p->s_prod[i % p->P];
+    const long M = (long)c.T * c.B;
+    const long ga = std::min(p->grows, M);
+    ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    int rc = ASR_OK;
+    if (ga > 0) {
+        ASR_HIP_TRY(hipStreamWaitEvent(p->s_gdec, p->ev_free[k], 0));
+        rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], (int)ga, c.in, c.H, ASR_EPI_NONE, p->s_gdec);
+        if (rc) return rc;
+        ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
+    }
+    if (ga < M)
+        rc = asr_linear_fwd(x + ga * c.in, p->W_ih, nullptr, p->hid[k] + ga * c.H, (int)(M - ga), c.in, c.H,
+                            ASR_EPI_NONE, sp);
+    if (rc) return rc;
+    if (ga > 0) ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_proj[k], 0));
+    rc = asr_rnn_emit_fwd(nullptr, p->W_hh, p->b_ih, p->b_hh, p->W_out, p->b_out, p->hid[k], nullptr, p->emis[k],
+                          c.T, c.B, c.H, c.V, sp);
     if (rc) return rc;
     ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
     return ASR_OK;
@@ -188,6 +227,7 @@ void release(asr_pipeline* p) {
     for (auto s : p->s_dec) if (s) hipStreamSynchronize(s);
     for (auto s : p->s_prod) if (s) hipStreamSynchronize(s);
     if (p->s_gemm) hipStreamSynchronize(p->s_gemm);
+    if (p->s_gdec) hipStreamSynchronize(p->s_gdec);
     for (auto h : p->dec) asr_ctc_destroy(h);
     for (auto b : p->hid) hipFree(b);
     for (auto b : p->emis) hipFree(b);
@@ -196,6 +236,7 @@ void release(asr_pipeline* p) {
     for (auto s : p->s_dec) if (s) hipStreamDestroy(s);
     for (auto s : p->s_prod) if (s) hipStreamDestroy(s);
     if (p->s_gemm) hipStreamDestroy(p->s_gemm);
+    if (p->s_gdec) hipStreamDestroy(p->s_gdec);
 }
 
 }  // namespace
@@ -249,6 +290,17 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         const int Dw = std::max(1, std::min(8, (16 * dc + c.B / 2) / c.B));   // 16 decodes per CU
         p->D = c.inflight ? c.inflight : Dw;
         p->P = c.prod_streams ? c.prod_streams : (part ? (p->D >= 4 ? 4 : 3) : 1);
+        // the fused recurrence + emission kernel (ASR_PIPELINE_FUSE=0: the
+        // recurrence and the emission GEMM separately, A/B), and the decode
+        // CUs' share of the input projection rows (ASR_PIPELINE_GSPLIT: a
+        // fraction of the rows, A/B)
+        const char* fe = getenv("ASR_PIPELINE_FUSE");
+        p->fuse = (c.H & 15) == 0 && c.V <= 32 && !(fe && fe[0] == '0');
+        if (p->fuse && p->dcus) {
+            const char* ge = getenv("ASR_PIPELINE_GSPLIT");
+            const double f = ge ? atof(ge) : 0.0;
+            p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
+        }
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
         p->gcu = bcu;
@@ -273,6 +325,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     if (p->mode == SHARED) {
         for (int d = 0; d < p->D; d++) mk(&p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
         for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->dcus, ncu);
+        if (p->grows > 0) mk(&p->s_gdec, 0, p->dcus);
     } else {
         for (int d = 0; d < p->D; d++)
             mk(&p->s_dec[d], p->gcu ? d * p->gcu : 0, p->gcu ? (d + 1) * p->gcu : ncu);
@@ -339,7 +392,7 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
         if (trace) lap("tail+decode", last);
         p->pending_tail = i;
     } else {
-        rc = produce_full(p, i, x);
+        rc = p->fuse ? produce_fused(p, i, x) : produce_full(p, i, x);
         if (trace) lap("produce", last);
         p->submitted = i + 1;
         if (!rc) rc = enqueue_decode(p, i);
@@ -393,6 +446,13 @@ int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod
     if (inflight) *inflight = p->D;
     if (prod_streams) *prod_streams = p->P;
     if (decode_cus) *decode_cus = p->mode == SHARED ? (p->dcus ? p->dcus : p->ncu) : (p->gcu ? p->gcu : p->ncu);
+    return ASR_OK;
+}
+
+int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows) {
+    if (!p) return ASR_ERR_ARG;
+    if (fused) *fused = p->fuse ? 1 : 0;
+    if (decode_cu_rows) *decode_cu_rows = p->fuse ? p->grows : 0;
     return ASR_OK;
 }
 

@@ -341,6 +341,16 @@ int asr_rnn_recur_fwd(const float* h0, const float* W_hh, const float* b_ih, con
     return rnn_recurrence(h0, W_hh, b_ih, b_hh, hid, T, B, H, asr_stream(s));
 }
 
+int asr_rnn_emit_fwd(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
+                     const float* W_out, const float* b_out, const float* P, float* hiddens,
+                     float* emis, int T, int B, int H, int V, asr_stream_t s) {
+    if (!W_hh || !b_ih || !b_hh || !W_out || !b_out || !P || !emis || T <= 0 || B <= 0 || H <= 0 || V <= 0)
+        return ASR_ERR_ARG;
+    if ((const float*)emis == P || (hiddens && (hiddens == emis || hiddens == h0))) return ASR_ERR_ARG;
+    return asr::rnn_emit_mfma_launch(h0, W_hh, b_ih, b_hh, P, hiddens, W_out, b_out, emis, T, B, H, V,
+                                     asr_stream(s));
+}
+
 size_t asr_rnn_bidir_workspace_bytes(int T, int B, int H) {
     if (T <= 0 || B <= 0 || H <= 0) return 0;
     return 2 * (size_t)T * B * H * sizeof(float);

@@ -133,6 +133,25 @@ int asr_rnn_recur_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_i
 enum { ASR_RNN_RECUR_AUTO = 0, ASR_RNN_RECUR_VALU = 1, ASR_RNN_RECUR_MFMA = 2 };
 int asr_rnn_set_recurrence(int kind);
 
+/* The recurrence and the emission layer in one pass — RNN::forward's
+ * recurrence (RNN.cu:9-30) followed by Linear::forward (Linear.cu:42-49) with
+ * the log_softmax of baseline/model.py:49, for the acoustic model's last RNN
+ * layer when H <= 256 (H % 16 == 0) and V <= 32:
+ *   h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)),
+ *   emis_t = log_softmax(h_t.W_out + b_out) per row.
+ * d_P [T*B, H] holds x.W_ih (read only; asr_linear_fwd(x, W_ih, NULL, P, ...,
+ * ASR_EPI_NONE)); d_emis [T*B, V]; d_hiddens [T*B, H] receives the hidden
+ * states, or NULL: they are never stored (the emission projection runs on
+ * the recurrence's matrix cores from on-chip h_t).  Always the MFMA
+ * recurrence (16 utterances per workgroup).  Emissions agree with
+ * asr_rnn_recur_fwd + asr_linear_fwd(..., ASR_EPI_BIAS_LOGSOFTMAX) to fp32
+ * rounding (another summation order of h.W_out), not bit for bit.
+ * ASR_ERR_UNSUPPORTED outside H <= 256, H % 16 == 0, V <= 32. */
+int asr_rnn_emit_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_ih,
+                     const float* d_b_hh, const float* d_W_out, const float* d_b_out,
+                     const float* d_P, float* d_hiddens, float* d_emis, int T, int B, int H,
+                     int V, asr_stream_t s);
+
 /* Bidirectional single-layer RNN — nn.RNN(bidirectional=True) of the Python
  * baseline (baseline/model.py:30, "bidir true"); the C++
  * RNN class (RNN.h:13-20) has no such mode, so this is an added entry point.
@@ -295,6 +314,15 @@ int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
  * utterance in the last decode.  Any pointer may be NULL. */
 int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod_streams, int* decode_cus,
                           int* decode_waves);
+/* How the pipeline produces a batch's emissions: fused = 1 when the
+ * recurrence and the emission projection + log_softmax run as one kernel
+ * (chip-filling batches with H % 16 == 0, V <= 32: asr_linear_fwd(x, W_ih,
+ * NULL, P, ..., ASR_EPI_NONE) then asr_rnn_emit_fwd(NULL, W_hh, b_ih, b_hh,
+ * W_out, b_out, P, NULL, emis, ...) gives its bits), 0 when it is
+ * asr_rnn_fwd then asr_linear_fwd(..., ASR_EPI_BIAS_LOGSOFTMAX);
+ * decode_cu_rows: input-projection rows run on the decode CUs.  Either
+ * pointer may be NULL. */
+int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows);
 int asr_pipeline_destroy(asr_pipeline_t* p);
 
 #ifdef __cplusplus

@@ -235,6 +235,61 @@ def test_rnn_forward_mfma_recurrence(T, B, I, H, monkeypatch):
     assert np.array_equal(hid2.toCpu(), got)
 
 
+@pytest.mark.parametrize("T,B,I,H,V", [(40, 37, 64, 256, 29), (1, 5, 16, 256, 29), (2, 16, 24, 48, 32),
+                                       (9, 33, 40, 80, 7), (5, 50, 8, 16, 1), (30, 256, 256, 256, 29)])
+def test_rnn_emit_fused(T, B, I, H, V, monkeypatch):
+    """asr_rnn_emit_fwd (recurrence + emission projection + log_softmax in
+    one kernel, hidden states optional) against torch.nn.RNN -> Linear ->
+    log_softmax in fp32 (tolerance 5e-5 * (1 + |ref|)), with and without h0,
+    ragged last utterance tile, odd wave counts, T = 1 and 2 (the pipelined
+    epilogue's edges); the stored hidden states are the MFMA recurrence's bits;
+    P is left unchanged."""
+    monkeypatch.setenv("ASR_RNN_MFMA", "1")
+    rng = np.random.default_rng(T * 13 + H + V)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    w_out = rng.uniform(-4 * s, 4 * s, (H, V)).astype(np.float32)
+    b_out = rng.uniform(-0.5, 0.5, V).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    W = [dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1))]
+    Wo, bo = dm(w_out), dm(b_out.reshape(V, 1))
+    for h0_np in (None, h0):
+        P = asr.DeviceMatrix(T * B, H)
+        asr.linear_fwd(dm(x), W[0], None, P, asr.EPI_NONE)
+        p_before = P.toCpu()
+        em, hid = asr.DeviceMatrix(T * B, V), asr.DeviceMatrix(T * B, H)
+        h0d = None if h0_np is None else dm(h0_np)
+        asr.rnn_emit_fwd(W[1], W[2], W[3], Wo, bo, P, em, T, B, h0=h0d, hid=hid)
+        href = _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0_np)
+        eref = torch.log_softmax(torch.from_numpy(href) @ torch.from_numpy(w_out) + torch.from_numpy(b_out),
+                                 dim=1).numpy()
+        close(em.toCpu(), eref, 5e-5)
+        assert np.array_equal(P.toCpu(), p_before)
+        # hidden states: the MFMA recurrence's own bits
+        hid2 = asr.DeviceMatrix(T * B, H)
+        asr.linear_fwd(dm(x), W[0], None, hid2, asr.EPI_NONE)
+        asr.rnn_recur_fwd(W[1], W[2], W[3], hid2, T, B, h0=h0d)
+        assert np.array_equal(hid.toCpu(), hid2.toCpu())
+        # without stored hiddens: the same emissions
+        em2 = asr.DeviceMatrix(T * B, V)
+        asr.rnn_emit_fwd(W[1], W[2], W[3], Wo, bo, P, em2, T, B, h0=h0d)
+        assert np.array_equal(em2.toCpu(), em.toCpu())
+
+
+def test_rnn_emit_unsupported_shapes():
+    """V > 32 or H > 256 or H % 16 != 0: ASR_ERR_UNSUPPORTED, nothing runs."""
+    for H, V in ((256, 33), (272, 29), (40, 29)):
+        P, em = asr.DeviceMatrix(4 * 2, H), asr.DeviceMatrix(4 * 2, V)
+        Wh, b = asr.DeviceMatrix(H, H), asr.DeviceMatrix(H, 1)
+        Wo, bo = asr.DeviceMatrix(H, V), asr.DeviceMatrix(V, 1)
+        with pytest.raises(Exception, match="asr_rnn_emit_fwd"):
+            asr.rnn_emit_fwd(Wh, b, b, Wo, bo, P, em, 4, 2)
+
+
 def test_rnn_recurrence_schedule_choice(monkeypatch):
     """Without the override the library picks the MFMA recurrence at
     B >= 4 x CUs (C4's one-GPU batch of 2048) and the VALU one below it; both

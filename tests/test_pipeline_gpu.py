@@ -22,12 +22,11 @@ def _weights(inp, H, V, seed):
     return [asr.DeviceMatrix.from_numpy(np.asarray(a, np.float32)) for a in host]
 
 
-def _sequential(x, W, T, B, inp, H, V, beam, recur):
+def _sequential(x, W, T, B, inp, H, V, beam, recur, fused=False):
     asr.rnn_set_recurrence(recur)
     try:
-        hid, em = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, V)
-        asr.rnn_fwd(x, W[0], W[1], W[2], W[3], hid, T, B)
-        asr.linear_fwd(hid, W[4], W[5], em, asr.EPI_BIAS_LOGSOFTMAX)
+        em = asr.DeviceMatrix(T * B, V)
+        asr.model_emissions(x, W, T, B, em, fused)
         dec = asr.CTCDecoder(V, beam, 0)
         dec.decode_device(em.ptr, T, B, is_log=True)
         lab, ln, lp = dec.best_arrays()
@@ -41,6 +40,7 @@ def _sequential(x, W, T, B, inp, H, V, beam, recur):
 @pytest.mark.parametrize("T,B,inp,H,V,beam,mode,recur", [
     (60, 16, 64, 64, 29, 10, "CU groups (small batches)", asr.RNN_RECUR_AUTO),
     (40, 256, 48, 64, 29, 50, "chip-filling batches", asr.RNN_RECUR_MFMA),
+    (40, 512, 48, 64, 47, 50, "chip-filling batches", asr.RNN_RECUR_MFMA),   # V > 32: not fused
     (20, 8, 32, 384, 29, 8, "CU groups (H > 256)", asr.RNN_RECUR_AUTO),
 ])
 def test_pipeline_matches_sequential(T, B, inp, H, V, beam, mode, recur):
@@ -70,7 +70,7 @@ def test_pipeline_matches_sequential(T, B, inp, H, V, beam, mode, recur):
     p.close()
     assert len(got) == len(xs)
     for i, x in enumerate(xs):
-        ref = _sequential(x, W, T, B, inp, H, V, beam, recur)
+        ref = _sequential(x, W, T, B, inp, H, V, beam, recur, d["fused_emission"])
         assert got[i][0] == ref[0], f"batch {i}: labels differ ({d})"
         assert np.array_equal(got[i][1], ref[1]), f"batch {i}: log-probs differ ({d})"
 
@@ -91,6 +91,33 @@ def test_pipeline_explicit_schedule_and_shared_cus():
         lab, ln, lp, _ = p.collect()
         outs.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
     p.close()
-    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA)
+    assert d["fused_emission"]   # chip-filling batch, V <= 32
+    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
     for o in outs:
         assert o[0] == ref[0] and np.array_equal(o[1], ref[1])
+
+
+@pytest.mark.parametrize("gsplit", ["0.3", "1.0"])
+def test_pipeline_input_projection_on_decode_cus(gsplit, monkeypatch):
+    """ASR_PIPELINE_GSPLIT: part (or all) of each batch's input projection on
+    the decode CUs' stream; rows are independent, so the results are the
+    sequential fused production's bits."""
+    monkeypatch.setenv("ASR_PIPELINE_GSPLIT", gsplit)
+    T, B, inp, H, V, beam = 24, 600, 64, 256, 29, 30
+    W = _weights(inp, H, V, seed=11)
+    rng = np.random.default_rng(5)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(4)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert d["mode"] == "chip-filling batches" and d["fused_emission"], d
+    assert d["decode_cu_gemm_rows"] == int(float(gsplit) * T * B) // 128 * 128, d
+    for x in xs:
+        p.submit(x)
+    got = []
+    while p.pending():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    p.close()
+    for g, x in zip(got, xs):
+        ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
