@@ -56,8 +56,10 @@ import numpy as np
 # GEMM streams of production exceed HIP's default of 4, and streams sharing a
 # queue run one after another (C5 with 5 streams on 4 queues: 1.03 M vs
 # 3.48 M frames/s, gpurun_out/r2g31).  Read when the HIP runtime starts.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# Small shards (C4 at N = 8: 256 utterances per GPU) keep 8 decodes and 8
+# productions in flight: 17 streams.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 try:
     import torch

@@ -634,8 +634,9 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 // recurrence's matrix cores: wave w contracts its own k-slice of h_t (the
 // chunks 2w, 2w + 1 it already reads as A fragments) with W_out[k-slice][32]
 // held in 16 VGPRs — 16 MFMAs beside its 128 recurrence MFMAs — and writes
-// the 16 x 32 partial to LDS; one step later the partials are summed in wave
-// order, biased and log-softmaxed per row (32 lanes per row), and stored.
+// the 16 x 32 partial to LDS; one step later waves 0-3 sum the partials in
+// wave order, add the bias and log-softmax each row with DPP reductions over
+// the 16 lanes that hold it, and store.
 // Pipelined: step t issues h_{t-1}'s partials and finishes h_{t-2}'s row.
 // The contraction order (8 partial chains, then a fixed sum) differs from the
 // GEMM kernels' single chain: emissions agree with asr_linear_fwd to fp32
@@ -645,8 +646,7 @@ constexpr int RM_ROWS = 16;
 constexpr int RM_LD = RNN_HMAX + 4;   // LDS row stride (floats): b128 reads of a quarter-wave hit distinct banks
 constexpr int RM_NCH = RNN_HMAX / 16;  // 16-k chunks at H = 256
 constexpr int RE_VMAX = 32;           // EMIT: vocabulary columns (two 16-column tiles)
-constexpr int RE_LD = 36;             // EMIT: partial row stride (floats): a wave's C-fragment stores hit distinct banks
-constexpr int RE_PART = (RNN_HMAX / 32) * RM_ROWS * RE_LD;   // EMIT: one buffer of 8 waves' 16 x 32 partials
+constexpr int RE_PART = (RNN_HMAX / 32) * RM_ROWS * RE_VMAX;   // EMIT: one buffer of 8 waves' 16 x 32 partials
 
 template <bool EMIT>
 __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __restrict__ h0,
@@ -707,8 +707,7 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
     float* const hdst = EMIT ? hout : hid;
     // EMIT: wo[ii][vt][e] = W_out[16 (2w + ii) + 4g + e][16 vt + c] (zero past H or V)
     float wo[2][2][4];
-    const int nw = (nch + 1) >> 1;
-    float bo = 0.f;
+    float bo0 = 0.f, bo1 = 0.f;
     if (EMIT) {
 #pragma unroll
         for (int ii = 0; ii < 2; ii++)
@@ -719,12 +718,14 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
                     const int k = 16 * (2 * w + ii) + 4 * g + e, col = 16 * vt + c;
                     wo[ii][vt][e] = (2 * w + ii < nch && col < V) ? Wout[(long)k * V + col] : 0.f;
                 }
-        bo = (lane & 31) < V ? bout[lane & 31] : 0.f;
+        bo0 = c < V ? bout[c] : 0.f;
+        bo1 = 16 + c < V ? bout[16 + c] : 0.f;
     }
-    // EMIT: wave w's partial of h_s . W_out over its k-slice (chunks 2w, 2w + 1)
-    // into partial buffer s & 1 (h_s in hs[buf])
-    auto emit_partial = [&](int buf, int s) {
-        f32x4 ea[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    // EMIT: wave w's partial of h . W_out over its k-slice (chunks 2w, 2w + 1
+    // of the h held in hs[buf])
+    auto emit_partial = [&](int buf, f32x4 (&ea)[2]) {
+        ea[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ea[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         const float* hr = &hs[buf][c * RM_LD + 4 * g];
 #pragma unroll
         for (int ii = 0; ii < 2; ii++) {
@@ -740,44 +741,68 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
                 }
             }
         }
-        float* pp = &ep[s & 1][w * RM_ROWS * RE_LD];
-#pragma unroll
-        for (int vt = 0; vt < 2; vt++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) pp[(4 * g + j) * RE_LD + 16 * vt + c] = ea[vt][j];
     };
-    // EMIT: emissions of frame s from partial buffer s & 1: thread (row, col)
-    // sums the waves' partials in wave order, + b_out, log_softmax over the
-    // row's 32 lanes (columns >= V are -inf), stores columns < V
-    auto emit_rows = [&](int s) {
+    // ... to partial buffer s & 1, in C-fragment order: [wave][j][lane][vt]
+    // (one ds_write_b64 per j, a wave's 64 lanes contiguous)
+    auto store_partial = [&](int s, const f32x4 (&ea)[2]) {
+        float* pp = &ep[s & 1][w * 4 * 128];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            *reinterpret_cast<float2*>(pp + j * 128 + 2 * lane) = float2{ea[0][j], ea[1][j]};
+    };
+    // EMIT: emissions of frame s from partial buffer s & 1.  Wave w < 4 owns
+    // the rows 4g + w of the tile (register j = w of the C fragments): lane
+    // (g, c) sums the waves' partials of its two columns c, 16 + c in wave
+    // order (absent waves' buffers hold zeros), + b_out, and the row's
+    // log_softmax over its 32 columns is a reduction over the 16 lanes of the
+    // lane group — one DPP row (quad_perm xor 1, xor 2, half-mirror, mirror),
+    // no LDS round trips.  Fewer than 4 waves (H < 128): a wave takes
+    // several j.
+    constexpr int NWMAX = RNN_HMAX / 32;
+    auto dpp_max16 = [](float x) {
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false)));
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false)));
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false)));
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false)));
+        return x;
+    };
+    auto dpp_sum16 = [](float x) {
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false));
+        return x;
+    };
+    const int nwblk = (int)blockDim.x >> 6;
+    auto emit_rows = [&](int s, bool store) {
         const float* pp = ep[s & 1];
-        for (int idx0 = 0; idx0 < RM_ROWS * 32; idx0 += (int)blockDim.x) {
-            const int idx = idx0 + tid;   // whole waves in or out of range (blockDim % 64 == 0)
-            const int row = idx >> 5, col = idx & 31;
-            float v = -INFINITY;
-            if (idx < RM_ROWS * 32 && col < V) {
-                float acc = 0.f;
-                for (int q = 0; q < nw; q++) acc += pp[(q * RM_ROWS + row) * RE_LD + col];
-                v = acc + bo;
+        for (int j = w; j < 4; j += nwblk) {
+            float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NWMAX; q++) {
+                const float2 x = *reinterpret_cast<const float2*>(pp + (q * 4 + j) * 128 + 2 * lane);
+                v0 += x.x;
+                v1 += x.y;
             }
-            float mx = v;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-            float se = col < V ? expf(v - mx) : 0.f;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) se += __shfl_xor(se, o);
+            v0 = c < V ? v0 + bo0 : -INFINITY;
+            v1 = 16 + c < V ? v1 + bo1 : -INFINITY;
+            const float mx = dpp_max16(fmaxf(v0, v1));
+            const float se = dpp_sum16((c < V ? expf(v0 - mx) : 0.f) + (16 + c < V ? expf(v1 - mx) : 0.f));
             const float lz = mx + logf(se);
-            if (idx < RM_ROWS * 32 && col < V && r0 + row < B)
-                emis[((long)s * B + r0 + row) * V + col] = v - lz;
+            const int row = r0 + 4 * g + j;
+            if (store && row < B) {
+                float* er = emis + ((long)s * B + row) * V;
+                if (c < V) er[c] = v0 - lz;
+                if (16 + c < V) er[16 + c] = v1 - lz;
+            }
         }
     };
+    if (EMIT) {
+        for (int x = tid; x < 2 * RE_PART; x += nthr) (&ep[0][0])[x] = 0.f;
+    }
     __syncthreads();
     int cur = 0;
     for (int t = 0; t < T; t++) {
-        if (EMIT) {
-            if (t >= 2) emit_rows(t - 2);
-            if (t >= 1) emit_partial(cur, t - 1);
-        }
         float p[2][4];
 #pragma unroll
         for (int tt = 0; tt < 2; tt++)
@@ -811,6 +836,15 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
                 }
             }
         }
+        if (EMIT) {
+            // beside this step's MFMAs: h_{t-1}'s partials (h_{t-1} is in
+            // hs[cur]; at t = 0 a dummy into the other buffer, never read)
+            // and h_{t-2}'s emissions (their partials were stored last step)
+            f32x4 ea[2];
+            emit_partial(cur, ea);
+            emit_rows(t - 2, t >= 2);
+            store_partial(t - 1 + 2, ea);
+        }
         float* hn = hs[cur ^ 1];
 #pragma unroll
         for (int tt = 0; tt < 2; tt++) {
@@ -827,10 +861,12 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
         lds_barrier();
     }
     if (EMIT) {   // the last two frames' emissions
-        if (T >= 2) emit_rows(T - 2);
-        emit_partial(cur, T - 1);
+        f32x4 ea[2];
+        emit_partial(cur, ea);   // h_{T-1}
+        if (T >= 2) emit_rows(T - 2, true);
+        store_partial(T - 1, ea);
         lds_barrier();
-        emit_rows(T - 1);
+        emit_rows(T - 1, true);
     }
 }
 

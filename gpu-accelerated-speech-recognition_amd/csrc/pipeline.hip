@@ -289,7 +289,10 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         const int dc = p->dcus ? p->dcus : ncu;
         const int Dw = std::max(1, std::min(8, (16 * dc + c.B / 2) / c.B));   // 16 decodes per CU
         p->D = c.inflight ? c.inflight : Dw;
-        p->P = c.prod_streams ? c.prod_streams : (part ? (p->D >= 4 ? 4 : 3) : 1);
+        // production streams: the recurrence of a batch is latency-bound
+        // (T steps) on B / 16 CUs, so as many batches produce at once as
+        // decode at once (small shards: 256 per GPU, D = 8 -> P = 8)
+        p->P = c.prod_streams ? c.prod_streams : (part ? std::max(3, p->D) : 1);
         // the fused recurrence + emission kernel (ASR_PIPELINE_FUSE=0: the
         // recurrence and the emission GEMM separately, A/B), and the decode
         // CUs' share of the input projection rows (ASR_PIPELINE_GSPLIT: a
@@ -298,7 +301,12 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->fuse = (c.H & 15) == 0 && c.V <= 32 && !(fe && fe[0] == '0');
         if (p->fuse && p->dcus) {
             const char* ge = getenv("ASR_PIPELINE_GSPLIT");
-            const double f = ge ? atof(ge) : 0.0;
+            // default 0.3 with one decode in flight (measured, C4 one GPU:
+            // 0 / 0.2 / 0.3 / 0.4 / 0.5 -> 176 / 198 / 202 / 196 / 191 M
+            // frames/s); with several in flight the next batch's decode
+            // fills the decode CUs and the rows only delay it (1024 per GPU:
+            // 180 vs 171 M at 0.3; profiles/r03/bench_scan.md)
+            const double f = ge ? atof(ge) : (p->D == 1 ? 0.3 : 0.0);
             p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
         }
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
