@@ -285,7 +285,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // many in flight (256 per GPU: 8), and as many production streams as
         // the recurrence's latency (T steps, whatever B) needs to keep up.
         const bool part = c.decode_cus != -1;
-        p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : ncu / 2 / 8 * 8) : 0;
+        // decode CUs: half of them, 3/8 for batches under 512 utterances,
+        // whose production costs more CU time per frame (the input GEMM of a
+        // short M; measured at 256 per GPU, 60 steps: 128 / 96 / 80 decode
+        // CUs 137-142 / 155-162 / 145 M frames/s; at 512: 128 / 96 CUs
+        // 183 / 168-182 M; profiles/r03/bench_scan.md)
+        const int dauto = (c.B < 512 ? ncu * 3 / 8 : ncu / 2) / 8 * 8;
+        p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : dauto) : 0;
         const int dc = p->dcus ? p->dcus : ncu;
         const int Dw = std::max(1, std::min(8, (16 * dc + c.B / 2) / c.B));   // 16 decodes per CU
         p->D = c.inflight ? c.inflight : Dw;
