@@ -325,7 +325,16 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->mode = SHARED;
         p->dcus = c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : 0;
         p->D = c.inflight ? c.inflight : 1;
-        p->P = c.prod_streams ? c.prod_streams : 1;
+        // two productions in flight beside the decode; for H <= 256 the
+        // MFMA recurrence (B / 16 CUs, its workgroups fit beside the decode's
+        // instead of one 1024-thread workgroup per utterance on every CU)
+        // with the emission layer fused when V <= 32
+        p->P = c.prod_streams ? c.prod_streams : 2;
+        if (c.H <= 256 && (c.H & 15) == 0) {
+            p->rnn_kind = ASR_RNN_RECUR_MFMA;
+            const char* fe = getenv("ASR_PIPELINE_FUSE");
+            p->fuse = c.V <= 32 && !(fe && fe[0] == '0');
+        }
     }
     if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
     // D decoding + P producing (+1: split production queues the next input

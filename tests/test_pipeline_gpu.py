@@ -41,6 +41,8 @@ def _sequential(x, W, T, B, inp, H, V, beam, recur, fused=False):
     (60, 16, 64, 64, 29, 10, "CU groups (small batches)", asr.RNN_RECUR_AUTO),
     (40, 256, 48, 64, 29, 50, "chip-filling batches", asr.RNN_RECUR_MFMA),
     (40, 512, 48, 64, 47, 50, "chip-filling batches", asr.RNN_RECUR_MFMA),   # V > 32: not fused
+    (30, 300, 32, 64, 29, 100, "chip-filling batches", asr.RNN_RECUR_MFMA),  # beam 100 (C3-like): fused
+    (12, 300, 32, 384, 47, 60, "chip-filling batches", asr.RNN_RECUR_AUTO),  # H > 256 (BL-like)
     (20, 8, 32, 384, 29, 8, "CU groups (H > 256)", asr.RNN_RECUR_AUTO),
 ])
 def test_pipeline_matches_sequential(T, B, inp, H, V, beam, mode, recur):
