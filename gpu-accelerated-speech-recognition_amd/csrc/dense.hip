@@ -970,27 +970,33 @@ int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b
 }
 
 // ---------------------------------------------------------------------------
-// One recurrence step on MFMA for H % 128 == 0 (C5: H = 1024):
+// One recurrence step on MFMA for H % 128 == 0 (C5: H = 1024, BL: 2048):
 // h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)) in place over P_t.
-// A workgroup owns a (16*RB rows) x 16 columns tile; its RSM_WAVES (8) waves
-// split K eight ways (H/8 each) so that one step costs ~H/8/4 dependent MFMAs
-// instead of the whole K chain.  No LDS staging: every wave issues all the
-// operand loads of its K slice before its first MFMA (h rows as float4, W_hh
-// columns as 64-B row segments), then one LDS exchange sums the eight
-// partial tiles in a fixed order.  k assignment inside a 16-k chunk: MFMA j
-// of lane group g = lane>>4 takes k = 4g + j for both operands (any
-// bijection is a valid contraction).  Grid (H/16, ceil(B/(16*RB))).
-template <int RB, int RSM_WAVES>
+// A workgroup owns a (16 RB rows) x (16 NT columns) tile; its 8 waves split
+// K eight ways (H/8 each) so that one step costs ~H/8/4 dependent MFMAs per
+// tile instead of the whole K chain.  No LDS staging: every wave issues the
+// operand loads of CH 16-k chunks of its K slice before their MFMAs (h rows
+// as float4, W_hh columns as 64-B row segments), then one LDS exchange sums
+// the eight partial tiles in a fixed order.  k assignment inside a 16-k
+// chunk: MFMA j of lane group g = lane>>4 takes k = 4g + j for both operands
+// (any bijection is a valid contraction).  Every output is the same chain
+// (its wave's k in order, then the 8 partials in wave order) for any (RB,
+// NT), so the tiling never changes a bit and can follow the shape: wider
+// tiles re-read h_{t-1} and W_hh fewer times (BL, B = 256, H = 2048:
+// 16-column tiles read 384 MB per step from L2 for a 2 GFLOP product).
+// Grid (H / (16 NT), ceil(B / (16 RB))).
+constexpr int RSM_WAVES = 8;
+template <int RB, int NT>
 __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __restrict__ ht,
                                                                       const float* __restrict__ hp,
                                                                       const float* __restrict__ Whh,
                                                                       const float* __restrict__ b_ih,
                                                                       const float* __restrict__ b_hh,
                                                                       int B, int H) {
-    __shared__ f32x4 part[RSM_WAVES][RB][64];
-    constexpr int CH = 8;   // 16-k chunks whose loads are in flight together
+    __shared__ f32x4 part[RSM_WAVES][RB * NT][64];
+    constexpr int CH = (RB * NT >= 4) ? 4 : 8;   // 16-k chunks whose loads are in flight together
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n0 = blockIdx.x * 16, r0 = blockIdx.y * (16 * RB);
+    const int n0 = blockIdx.x * (16 * NT), r0 = blockIdx.y * (16 * RB);
     const int g = lane >> 4, c = lane & 15;
     const int kw = H / RSM_WAVES, kbeg = w * kw, nchunk = kw / 16;
     const float* arow[RB];
@@ -1000,12 +1006,14 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __
         arow[rb] = hp + (long)r * H + kbeg + 4 * g;
     }
     const float* bcol = Whh + (long)(kbeg + 4 * g) * H + n0 + c;
-    f32x4 acc[RB];
+    f32x4 acc[RB][NT];
 #pragma unroll
-    for (int rb = 0; rb < RB; rb++) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) acc[rb][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ch0 = 0; ch0 < nchunk; ch0 += CH) {
         float4 a[CH][RB];
-        float b[CH][4];
+        float b[CH][NT][4];
 #pragma unroll
         for (int i = 0; i < CH; i++) {
             if (ch0 + i < nchunk) {
@@ -1013,51 +1021,77 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __
 #pragma unroll
                 for (int rb = 0; rb < RB; rb++) a[i][rb] = *reinterpret_cast<const float4*>(arow[rb] + k);
 #pragma unroll
-                for (int j = 0; j < 4; j++) b[i][j] = bcol[(long)(k + j) * H];
+                for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) b[i][nt][j] = bcol[(long)(k + j) * H + 16 * nt];
             }
         }
 #pragma unroll
         for (int i = 0; i < CH; i++) {
             if (ch0 + i < nchunk) {
 #pragma unroll
-                for (int rb = 0; rb < RB; rb++) {
-                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].x, b[i][0], acc[rb], 0, 0, 0);
-                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].y, b[i][1], acc[rb], 0, 0, 0);
-                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].z, b[i][2], acc[rb], 0, 0, 0);
-                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].w, b[i][3], acc[rb], 0, 0, 0);
-                }
+                for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+                    for (int nt = 0; nt < NT; nt++) {
+                        f32x4& q = acc[rb][nt];
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].x, b[i][nt][0], q, 0, 0, 0);
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].y, b[i][nt][1], q, 0, 0, 0);
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].z, b[i][nt][2], q, 0, 0, 0);
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].w, b[i][nt][3], q, 0, 0, 0);
+                    }
             }
         }
     }
 #pragma unroll
-    for (int rb = 0; rb < RB; rb++) part[w][rb][lane] = acc[rb];
-    __syncthreads();
-    // thread -> (rb, j, lane) of the tile; the C/D layout of 16x16 tiles:
-    // element j of lane l is row (l>>4)*4 + j, column l & 15.
-    for (int e = tid; e < RB * 256; e += 64 * RSM_WAVES) {
-        const int rb = e >> 8, j = (e >> 6) & 3, l = e & 63;
-        const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + (l & 15);
-        if (r >= B) continue;
-        float hh = part[0][rb][l][j];
+    for (int rb = 0; rb < RB; rb++)
 #pragma unroll
-        for (int q = 1; q < RSM_WAVES; q++) hh += part[q][rb][l][j];
+        for (int nt = 0; nt < NT; nt++) part[w][rb * NT + nt][lane] = acc[rb][nt];
+    __syncthreads();
+    // thread -> (tile, j, lane) of the 16x16 tiles; the C/D layout: element j
+    // of lane l is row (l>>4)*4 + j, column l & 15.
+    for (int e = tid; e < RB * NT * 256; e += 64 * RSM_WAVES) {
+        const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
+        const int rb = tl / NT, nt = tl - rb * NT;
+        const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
+        if (r >= B) continue;
+        float hh = part[0][tl][l][j];
+#pragma unroll
+        for (int q = 1; q < RSM_WAVES; q++) hh += part[q][tl][l][j];
         float* out = ht + (long)r * H + n;
         *out = tanhf((*out + hh) + (b_hh[n] + b_ih[n]));
     }
+}
+
+template <int RB, int NT>
+static void launch_step_mfma(float* ht, const float* hp, const float* Whh, const float* b_ih, const float* b_hh,
+                             int B, int H, hipStream_t s) {
+    hipLaunchKernelGGL((rnn_step_mfma_kernel<RB, NT>), dim3((unsigned)(H / (16 * NT)), (unsigned)((B + 16 * RB - 1) / (16 * RB))),
+                       dim3(64 * RSM_WAVES), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
 }
 
 int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                          const float* b_hh, int B, int H, hipStream_t s) {
     if (B <= 0 || H <= 0 || (H % 128) != 0) return ASR_ERR_UNSUPPORTED;
     if ((uintptr_t)hp % 16 != 0) return ASR_ERR_UNSUPPORTED;   // float4 rows
-    const unsigned nb16 = (unsigned)((B + 15) / 16);
-    if ((unsigned)(H / 16) * nb16 <= 512) {   // 16-row tiles while that is <= 2 per CU
-        hipLaunchKernelGGL((rnn_step_mfma_kernel<1, 8>), dim3((unsigned)(H / 16), nb16),
-                           dim3(64 * 8), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
+    // ASR_RNN_STEP_NT=1/2/4 forces the column tiles per workgroup (A/B)
+    const char* fe = getenv("ASR_RNN_STEP_NT");
+    int nt = fe ? atoi(fe) : 0;
+    const long nb16 = (B + 15) / 16, nb32 = (B + 31) / 32;
+    if (nt != 1 && nt != 2 && nt != 4) {
+        // the widest tiles that still give every CU a workgroup (256 CUs:
+        // BL's 256 x 2048 -> 32 x 8 = 256 workgroups of 32 x 64); narrow
+        // tiles for small B (C5's 32 x 1024: latency-bound, 64 x 2)
+        nt = (H / 64) * nb32 >= 256 ? 4 : ((H / 32) * nb32 >= 256 ? 2 : 1);
+    }
+    if (nt == 4) {
+        launch_step_mfma<2, 4>(ht, hp, Whh, b_ih, b_hh, B, H, s);
+    } else if (nt == 2) {
+        launch_step_mfma<2, 2>(ht, hp, Whh, b_ih, b_hh, B, H, s);
+    } else if ((H / 16) * nb16 <= 512) {   // 16-row tiles while that is <= 2 per CU
+        launch_step_mfma<1, 1>(ht, hp, Whh, b_ih, b_hh, B, H, s);
     } else {   // 32-row tiles (measured: 16-row tiles win up to ~2 workgroups per CU, 64-row
                // tiles and 16 waves per workgroup lose everywhere)
-        hipLaunchKernelGGL((rnn_step_mfma_kernel<2, 8>), dim3((unsigned)(H / 16), (unsigned)((B + 31) / 32)),
-                           dim3(64 * 8), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
+        launch_step_mfma<2, 1>(ht, hp, Whh, b_ih, b_hh, B, H, s);
     }
     ASR_LAUNCH_TRY();
     return ASR_OK;

@@ -368,6 +368,32 @@ def test_rnn_forward_mfma_step(T, B, H):
     close(hid.toCpu(), _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
 
 
+@pytest.mark.parametrize("T,B,H", [(5, 256, 2048), (4, 37, 512), (3, 100, 1024)])
+def test_rnn_step_tilings_same_bits(T, B, H, monkeypatch):
+    """The H > 256 MFMA step with 1, 2 or 4 16-column tiles per workgroup
+    (ASR_RNN_STEP_NT; the automatic choice follows the shape: BL's 256 x
+    2048 takes 4) gives the same bits, and agrees with torch fp32."""
+    monkeypatch.setenv("ASR_RNN_GRAPH", "0")   # a captured graph would keep the first tiling
+    rng = np.random.default_rng(T + B + H)
+    I = 32
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    W = [dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1))]
+    outs = []
+    for nt in ("1", "2", "4", ""):
+        monkeypatch.setenv("ASR_RNN_STEP_NT", nt)
+        hid = asr.DeviceMatrix(T * B, H)
+        asr.rnn_fwd(dm(x), *W, hid, T, B)
+        outs.append(hid.toCpu())
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    close(outs[0], _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 1e-4)
+
+
 def test_rnn_multilayer():
     """num_layers > 1 (RNN.h:13-20): layer l+1 consumes layer l's hiddens."""
     T, B, I, H, L = 15, 6, 40, 64, 3
