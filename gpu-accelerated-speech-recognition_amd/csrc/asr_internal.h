@@ -32,6 +32,10 @@ static inline hipStream_t asr_stream(asr_stream_t s) { return (hipStream_t)s; }
 // the process-wide asr_rnn_set_recurrence choice).  Set by the pipeline
 // around its production so that it never changes the process-wide state.
 extern thread_local int asr_internal_rnn_kind;
+// Set by the pipeline around GEMMs that share CUs with decodes: use the tiled
+// kernel (short-lived workgroups) instead of the persistent wide one, so that
+// a decode launched meanwhile waits at most one tile for its CUs.  Same bits.
+extern thread_local int asr_internal_gemm_tiled;
 
 // Order-preserving bijection fp64 <-> u64: a < b  <=>  key(a) < key(b).
 // -0.0 is folded onto +0.0 (they compare equal as doubles).  Key 0 is never

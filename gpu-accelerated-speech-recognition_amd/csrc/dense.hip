@@ -392,6 +392,7 @@ static int launch_gemm_wide_k(const GemmArgs& g, hipStream_t s) {
 
 // ASR_GEMM_WIDE=0: the tiled kernel instead (A/B runs).
 static bool wide_off() {
+    if (asr_internal_gemm_tiled) return true;
     const char* e = getenv("ASR_GEMM_WIDE");
     return e && e[0] == '0';
 }

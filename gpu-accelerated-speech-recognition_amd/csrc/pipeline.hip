@@ -65,6 +65,7 @@ struct asr_pipeline {
     bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
     bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
+    bool gtiled = false;  // ... with the tiled GEMM kernel (several decodes in flight)
     hipStream_t s_gdec = nullptr;   // the decode CUs' share of the input projections
     std::vector<float*> hid, emis;
     std::vector<asr_ctc_t*> dec;
@@ -125,7 +126,12 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
     int rc = ASR_OK;
     if (ga > 0) {
         ASR_HIP_TRY(hipStreamWaitEvent(p->s_gdec, p->ev_free[k], 0));
+        // with several decodes in flight the decode-side rows use the tiled
+        // kernel: a decode launched meanwhile then waits at most one tile's
+        // workgroups for its CUs, not a persistent workgroup's whole share
+        asr_internal_gemm_tiled = p->gtiled ? 1 : 0;
         rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], (int)ga, c.in, c.H, ASR_EPI_NONE, p->s_gdec);
+        asr_internal_gemm_tiled = 0;
         if (rc) return rc;
         ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
     }
@@ -307,13 +313,17 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->fuse = (c.H & 15) == 0 && c.V <= 32 && !(fe && fe[0] == '0');
         if (p->fuse && p->dcus) {
             const char* ge = getenv("ASR_PIPELINE_GSPLIT");
-            // default 0.3 with one decode in flight (measured, C4 one GPU:
-            // 0 / 0.2 / 0.3 / 0.4 / 0.5 -> 176 / 198 / 202 / 196 / 191 M
-            // frames/s); with several in flight the next batch's decode
-            // fills the decode CUs and the rows only delay it (1024 per GPU:
-            // 180 vs 171 M at 0.3; profiles/r03/bench_scan.md)
-            const double f = ge ? atof(ge) : (p->D == 1 ? 0.3 : 0.0);
+            // default 0.3 (measured, C4 one GPU: 0 / 0.2 / 0.3 / 0.4 / 0.5 ->
+            // 176 / 198 / 202 / 196 / 191 M frames/s).  With several decodes
+            // in flight the rows run on the tiled GEMM kernel (below): with
+            // the persistent one a decode launched meanwhile waited for its
+            // CUs (1024 per GPU: 171 vs 180 M at 0.3 / 0), with the tiled one
+            // 0 / 0.2 / 0.3 -> 173 / 196 / 198 M, 512 per GPU 167 / 182 / 182 M
+            // (profiles/r03/bench_scan.md)
+            const double f = ge ? atof(ge) : 0.3;
             p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
+            const char* gt = getenv("ASR_PIPELINE_GTILED");   // A/B: 1 / 0 force, default: D > 1
+            p->gtiled = gt ? atoi(gt) != 0 : p->D > 1;
         }
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;

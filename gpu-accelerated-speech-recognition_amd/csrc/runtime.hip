@@ -20,6 +20,7 @@ thread_local std::string g_last_error;
 }
 
 thread_local int asr_internal_rnn_kind = -1;
+thread_local int asr_internal_gemm_tiled = 0;
 
 void asr_internal_set_error(const char* what, const char* msg, const char* file, int line) {
     char buf[512];
