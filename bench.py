@@ -311,6 +311,9 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--decode-only", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full-T", action="store_true",
+                    help="CPU baseline / parity sample over all T frames at any shape (default: all of "
+                         "them when that is ~20 s of CPU work, as at C4; a prefix otherwise)")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the rank-0 1-GPU re-decode of the gathered shards")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -763,7 +766,8 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                 xg = DM(make_features(T, nb, In, f))
                 em_g = asr.DeviceMatrix(T * nb, V)
                 asr.model_emissions(xg, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, nb, em_g,
-                                    bool((sched or {}).get("fused_emission")))
+                                    bool((sched or {}).get("fused_emission")),
+                                    recurrence=(sched or {}).get("recurrence"))
                 dg = asr.CTCDecoder(V, beam, 0, waves=args.waves)
                 dg.decode_device(em_g.ptr, T, nb, is_log=True)
                 lab1, lp1 = dg.best()
@@ -808,8 +812,15 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                              fused=(d_whh, d_bih, d_bhh) if (sched or {}).get("fused_emission") else None)
 
     cpu = None
+    parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam, d_emis_last)
+        if isinstance(d_emis_last, tuple):   # (host emissions, how they were obtained)
+            emis_host, note = d_emis_last
+        else:
+            emis_host, note = d_emis_last.toCpu(), "the decoded buffer of the timed region's last batch"
+        cpu = cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam, emis_host,
+                           best, full_T=args.cpu_full_T, emis_note=note)
+        parity = cpu.pop("parity")
 
     if rank == 0:
         line = {
@@ -828,11 +839,14 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
                        "decode_waves": dec_config[1],   # the schedule the decodes ran
                        **sched},
-            "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "gather": gather,
+            "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "parity": parity, "gather": gather,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and parity.get("checked") and not parity.get("match"):
+        raise SystemExit(f"parity: the measured path's results differ from the oracle on utterances "
+                         f"{parity.get('mismatched_ids')}")
 
 
 def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, weights):
@@ -898,16 +912,28 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     lab, ln, lp = (a.copy() for a in best["arrays"])
     Kb = beam + 1
     kcap = -(-(Kb + max(8, Kb // 8)) // 32) * 32
-    # buffers for the GEMM timing and one batch's real emissions for the CPU baseline
+    # buffers for the GEMM timing
     hid0, em0 = asr.DeviceMatrix(T * B, H), asr.DeviceMatrix(T * B, V)
-    em_real = asr.DeviceMatrix(T * B, V)
     fused = desc["fused_emission"]
+    em_last = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        asr.model_emissions(d_x, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, B, em_real, fused, work=hid0)
+        # the exact bytes the last collected batch's decode consumed (the
+        # parity witness of the measured path), and a check that
+        # model_emissions reproduces them (the 1-GPU re-decode relies on it)
+        em_last = pl.peek_emissions()
+        asr.model_emissions(d_x, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, B, em0, fused, work=hid0,
+                            recurrence=desc["recurrence"])
+        same = bool(np.array_equal(em0.toCpu().reshape(T, B, V), em_last))
+        em_last = (em_last, "the pipeline's own emission buffer of the timed region's last batch "
+                            "(asr_pipeline_peek_emissions); model_emissions reproduces it bit for bit: "
+                            + ("yes" if same else "NO"))
+        if not same:
+            raise SystemExit("model_emissions does not reproduce the pipeline's emissions")
     finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
-           (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_real,
+           (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_last,
            {"inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
             "decode_cus": desc["decode_cus"], "fused_emission": fused,
+            "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
@@ -1100,24 +1126,61 @@ def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V
     return out
 
 
-def cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam, d_emis):
+def parity_sample_ids(B: int, S: int):
+    """S utterance ids spread evenly over [0, B) (first and last included)."""
+    return sorted({int(round(v)) for v in np.linspace(0, B - 1, max(1, min(S, B)))})
+
+
+def cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam, emis_host, best,
+                 full_T=False, emis_note=""):
     """The CPU restatement of CTCBeamSearch.cpp (oracle/ctc_oracle.cpp, the
     reference's std::set/std::map algorithm with fixes F1-F3 in fp64 log
-    domain) timed on this host's allotted cores over a bounded sample of the
-    same emissions, plus the same at C4's T=1000 shape (where north_star states
-    the >= 10x target).  Decoder only: the reference has no CPU RNN."""
+    domain, CTCBeamSearch.cpp:50-187) timed on this host's allotted cores over
+    a bounded sample of the emissions the timed region's last batch decoded
+    (emis_host [T][B][V]): one utterance per thread, spread over the batch.
+    When the sample covers every frame (C4: T = 1000) the oracle's answers
+    are also the parity witness of the measured path: each sampled
+    utterance's best labels must equal the GPU's (`best` = that batch's
+    collected labels / lengths / fp64 log-probs) and its log-prob agree to
+    1e-9 relative (the tests' tolerance; north_star asks 1e-4).  Decoder
+    only: the reference has no CPU RNN."""
     oracle = _load("ctc_oracle", ROOT / "oracle" / "ctc_oracle.py")
     threads, quota = cpu_share()
-    S = min(B, threads)
-    emis = d_emis.toCpu().reshape(T, B, V)[:, :S, :].copy()
-    Ts = min(T, max(4, int(2.0e7 / (S * (beam + 1) * (V + 1)))))   # C5: a prefix of the frames
-    secs = oracle.time_decode(emis[:Ts], beam, 0, is_log=True, nthreads=threads)
+    ids = parity_sample_ids(B, threads)
+    S = len(ids)
+    emis = np.ascontiguousarray(emis_host.reshape(T, B, V)[:, ids, :])
+    # ~20 s of CPU at C4's shape; longer shapes decode a prefix of the frames
+    # (C5), unless --cpu-full-T
+    Ts = T if full_T else min(T, max(4, int(2.6e7 / (S * (beam + 1) * (V + 1)))))
+    t0 = time.perf_counter()
+    ref = oracle.decode(emis[:Ts], beam, 0, is_log=True, nthreads=threads, max_hyps=1)
+    secs = time.perf_counter() - t0
     out = {"value": round(S * Ts / secs, 1), "unit": "frames/s", "cores": threads, "kind": "port",
            "model": cpu_model(), "host_cpus": os.cpu_count(), "cgroup_quota_cpus": quota,
            "per_core": round(S * Ts / secs / min(S, threads), 1),
-           "sample": f"oracle/ctc_oracle.cpp decode of {S} utterances x {Ts} frames of this run's "
-                     f"emissions (beam={beam}, V={V}), {threads} std::threads (one utterance each), "
-                     f"{secs:.2f} s wall; decoder only (the reference has no CPU RNN)"}
+           "sample": f"oracle/ctc_oracle.cpp decode of {S} utterances (ids spread over the batch) x {Ts} "
+                     f"frames of the emissions the timed region's last batch decoded (beam={beam}, V={V}), "
+                     f"{threads} std::threads (one utterance each), {secs:.2f} s wall; decoder only "
+                     f"(the reference has no CPU RNN)"}
+    parity = {"utterances": S, "frames": Ts, "checked": Ts == T}
+    if Ts == T:
+        lab, ln, lp = best
+        bad, worst = [], 0.0
+        for i, u in enumerate(ids):
+            rl, rlp = ref[i][0]
+            got = lab[u, :int(ln[u])].tolist()
+            err = abs(float(lp[u]) - rlp) / max(1.0, abs(rlp))
+            worst = max(worst, err)
+            if got != [int(c) for c in rl] or not err <= 1e-9:
+                bad.append(u)
+        parity.update({"match": not bad, "mismatched_ids": bad[:8], "max_logp_rel_err": worst,
+                       "ids": ids if S <= 16 else ids[:8] + ["..."],
+                       "tolerance": "best labels identical, |dlogp| <= 1e-9 max(1, |logp|)",
+                       "emissions": emis_note or "the emissions the decode consumed",
+                       "checker": "oracle/ctc_oracle.cpp (CTCBeamSearch.cpp:50-187, F1-F3, fp64 log domain)"})
+    else:
+        parity["note"] = f"the CPU sample is a {Ts}-frame prefix of T={T}: no parity claim from it"
+    out["parity"] = parity
     if V == 29 and beam == 50 and T != 1000:
         # C4 shape (T=1000, beam=50): emissions from the same model at T=1000
         T4 = 1000

@@ -17,6 +17,7 @@ libasr_amd.so is missing raises, there is no fallback path.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 from pathlib import Path
@@ -54,9 +55,11 @@ EXPORTS = [
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
-    "asr_ctc_set_concurrency", "asr_rnn_set_recurrence",
+    "asr_ctc_set_concurrency", "asr_rnn_set_recurrence", "asr_rnn_get_recurrence",
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
-    "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_destroy",
+    "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams",
+    "asr_pipeline_peek_emissions",
+    "asr_pipeline_destroy",
 ]
 
 
@@ -110,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_set_recurrence": [_i],
+        "asr_rnn_get_recurrence": [ctypes.POINTER(_i)],
         "asr_rnn_emit_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_pipeline_create": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)],
         "asr_pipeline_submit": [_vp, _vp],
@@ -118,7 +122,10 @@ def lib() -> ctypes.CDLL:
         "asr_pipeline_describe": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
                                   ctypes.POINTER(_i)],
         "asr_pipeline_destroy": [_vp],
-        "asr_pipeline_get_production": [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_longlong)],
+        "asr_pipeline_get_production": [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_longlong),
+                                        ctypes.POINTER(_i)],
+        "asr_pipeline_get_streams": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)],
+        "asr_pipeline_peek_emissions": [_vp, ctypes.POINTER(_vp)],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -299,6 +306,13 @@ RNN_RECUR_AUTO, RNN_RECUR_VALU, RNN_RECUR_MFMA = 0, 1, 2
 def rnn_set_recurrence(kind: int) -> None:
     """Process-wide recurrence kernel choice (asr_rnn_set_recurrence)."""
     check(lib().asr_rnn_set_recurrence(int(kind)), "asr_rnn_set_recurrence")
+
+
+def rnn_get_recurrence() -> int:
+    """The process-wide recurrence kernel choice (asr_rnn_get_recurrence)."""
+    k = _i()
+    check(lib().asr_rnn_get_recurrence(ctypes.byref(k)), "asr_rnn_get_recurrence")
+    return k.value
 
 
 def rnn_cell_fwd(x: DeviceMatrix, h_prev: DeviceMatrix, W_ih: DeviceMatrix,
@@ -507,20 +521,32 @@ PIPELINE_MODES = {0: "CU groups (small batches)", 1: "chip-filling batches", 2: 
 
 
 def model_emissions(x: "DeviceMatrix", weights, T: int, B: int, emis: "DeviceMatrix", fused: bool,
-                    work: Optional["DeviceMatrix"] = None, stream: int = 0) -> "DeviceMatrix":
+                    work: Optional["DeviceMatrix"] = None, stream: int = 0,
+                    recurrence: Optional[int] = None) -> "DeviceMatrix":
     """One batch's emissions the way a Pipeline produces them
     (asr_pipeline_get_production): fused — input projection GEMM, then the
     recurrence with the emission layer fused (asr_rnn_emit_fwd); otherwise
-    asr_rnn_fwd then asr_linear_fwd(..., log_softmax).  weights = (W_ih, W_hh,
-    b_ih, b_hh, W_out, b_out); work [T*B, H] is scratch (allocated if None)."""
+    asr_rnn_fwd then asr_linear_fwd(..., log_softmax), with the recurrence
+    kind the pipeline pinned (`recurrence`, Pipeline.describe()["recurrence"];
+    None / AUTO: the process-wide choice), restored afterwards.  weights =
+    (W_ih, W_hh, b_ih, b_hh, W_out, b_out); work [T*B, H] is scratch
+    (allocated if None)."""
     W_ih, W_hh, b_ih, b_hh, W_out, b_out = weights
     work = work if work is not None else DeviceMatrix(T * B, W_hh.cols)
     if fused:
         linear_fwd(x, W_ih, None, work, EPI_NONE, stream)
         rnn_emit_fwd(W_hh, b_ih, b_hh, W_out, b_out, work, emis, T, B, stream=stream)
-    else:
+        return emis
+    prev = None
+    if recurrence not in (None, RNN_RECUR_AUTO):
+        prev = rnn_get_recurrence()
+        rnn_set_recurrence(recurrence)
+    try:
         rnn_fwd(x, W_ih, W_hh, b_ih, b_hh, work, T, B, stream=stream)
-        linear_fwd(work, W_out, b_out, emis, EPI_BIAS_LOGSOFTMAX, stream)
+    finally:
+        if prev is not None:
+            rnn_set_recurrence(prev)
+    linear_fwd(work, W_out, b_out, emis, EPI_BIAS_LOGSOFTMAX, stream)
     return emis
 
 
@@ -543,20 +569,32 @@ class Pipeline:
         self._lab = np.zeros((B, max(T, 1)), np.int32)
         self._len = np.zeros(B, np.int32)
         self._lp = np.zeros(B, np.float64)
+        self._inputs = collections.deque()   # submitted features, alive until their batch is collected
+        self._kept = []                      # features of failed submits (alive until close)
 
     def describe(self):
         m, d, p, c, w = _i(), _i(), _i(), _i(), _i()
         check(lib().asr_pipeline_describe(self.h, ctypes.byref(m), ctypes.byref(d), ctypes.byref(p),
                                           ctypes.byref(c), ctypes.byref(w)), "asr_pipeline_describe")
-        fz, gr = _i(), ctypes.c_longlong()
-        check(lib().asr_pipeline_get_production(self.h, ctypes.byref(fz), ctypes.byref(gr)),
+        fz, gr, rk = _i(), ctypes.c_longlong(), _i()
+        check(lib().asr_pipeline_get_production(self.h, ctypes.byref(fz), ctypes.byref(gr), ctypes.byref(rk)),
               "asr_pipeline_get_production")
+        ns, hq = _i(), _i()
+        check(lib().asr_pipeline_get_streams(self.h, ctypes.byref(ns), ctypes.byref(hq)), "asr_pipeline_get_streams")
         return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
                 "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
-                "decode_cu_gemm_rows": gr.value}
+                "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
+                "hw_queues": hq.value}
 
     def submit(self, x: "DeviceMatrix") -> None:
-        check(lib().asr_pipeline_submit(self.h, x.ptr), "asr_pipeline_submit")
+        """Queue a batch.  x is kept alive here until its batch is collected
+        (asr_pipeline_submit reads it until then); after a failed submit it
+        is kept until close(): queued work of the batch may still read it."""
+        rc = lib().asr_pipeline_submit(self.h, x.ptr)
+        if rc != ASR_OK:
+            self._kept.append(x)
+            check(rc, "asr_pipeline_submit")
+        self._inputs.append(x)
 
     def pending(self) -> int:
         n = _i()
@@ -567,14 +605,30 @@ class Pipeline:
         """(labels [B][T] int32, lengths [B], logp [B] fp64, decode_ms) of the
         oldest batch; the arrays are reused by the next call."""
         ms = _f()
-        check(lib().asr_pipeline_collect(self.h, _ptr(self._lab), self._lab.shape[1], _ptr(self._len),
-                                         _ptr(self._lp), ctypes.byref(ms)), "asr_pipeline_collect")
+        rc = lib().asr_pipeline_collect(self.h, _ptr(self._lab), self._lab.shape[1], _ptr(self._len),
+                                        _ptr(self._lp), ctypes.byref(ms))
+        n = _i()
+        if lib().asr_pipeline_pending(self.h, ctypes.byref(n)) == ASR_OK:
+            while len(self._inputs) > n.value:   # collected batches' features may go
+                self._inputs.popleft()
+        check(rc, "asr_pipeline_collect")
         return self._lab, self._len, self._lp, ms.value
+
+    def peek_emissions(self) -> np.ndarray:
+        """Host copy of the emissions [T][B][V] the last collected batch's
+        decode consumed (asr_pipeline_peek_emissions)."""
+        ptr = _vp()
+        check(lib().asr_pipeline_peek_emissions(self.h, ctypes.byref(ptr)), "asr_pipeline_peek_emissions")
+        out = np.empty((self.T, self.B, self.cfg.V), np.float32)
+        check(lib().asr_memcpy_d2h(_ptr(out), ptr.value, out.nbytes, None), "asr_memcpy_d2h")
+        return out
 
     def close(self) -> None:
         if getattr(self, "h", None):
-            lib().asr_pipeline_destroy(self.h)
+            lib().asr_pipeline_destroy(self.h)   # synchronises the pipeline's streams
             self.h = None
+        self._inputs = collections.deque()
+        self._kept = []
 
     def __del__(self):
         try:

@@ -299,9 +299,12 @@ __global__ __launch_bounds__(64 * GW_W) void gemm_wide_kernel(GemmArgs g) {
     const int r = lane & 15, gq = lane >> 4;
     const int n0 = blockIdx.y * BNW;
     const int K = g.K;
-    for (int idx = tid; idx < K * BNW; idx += 64 * GW_W) {   // B^T slice, zero past N
+    // B^T slice, zero past N and past K: the MFMA loop always runs KMAX / 16
+    // chunks, and LDS left over from an earlier kernel (e.g. a decoder's u32
+    // keys, NaN as floats) times a zero A element would still be NaN
+    for (int idx = tid; idx < KMAX * BNW; idx += 64 * GW_W) {
         const int k = idx / BNW, n = idx - k * BNW;
-        Bt[n * BTS + k] = n0 + n < g.N ? g.B[(long)k * g.sbk + n0 + n] : 0.f;
+        Bt[n * BTS + k] = (k < K && n0 + n < g.N) ? g.B[(long)k * g.sbk + n0 + n] : 0.f;
     }
     const int ntile = (g.M + 16 * GW_W - 1) / (16 * GW_W);
     int tile = blockIdx.x;

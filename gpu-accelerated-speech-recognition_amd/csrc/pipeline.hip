@@ -53,6 +53,7 @@ struct Result {
     std::vector<double> lp;
     float ms = 0.f;
     int rc = ASR_OK;
+    long batch = -1;
 };
 
 }  // namespace
@@ -75,9 +76,31 @@ struct asr_pipeline {
     long submitted = 0, decoded = 0, collected = 0;
     long pending_tail = -1;   // split production: batch whose emission GEMM and decode are not queued yet
     std::deque<Result> stash;
+    long returned = -1;   // the batch the last asr_pipeline_collect returned
+    // A batch accepted by submit whose remaining work (emission GEMM, decode)
+    // then failed to queue can never return results: from it on the pipeline
+    // is failed, and every later submit / collect returns fail_rc.
+    long fail_from = -1;
+    int fail_rc = ASR_OK;
+    int hw_queues = 4, streams = 0;   // HIP hardware queues of the process, streams created
+    // test hook (ASR_PIPELINE_FAULT=<batch>:<stage>, stage head|tail|produce|decode):
+    // the named stage of that batch returns ASR_ERR_INTERNAL instead of queueing
+    long fault_batch = -1;
+    char fault_stage[8] = {0};
 };
 
 namespace {
+
+bool fault(asr_pipeline* p, long i, const char* stage) {   // fires once
+    if (i != p->fault_batch || std::strcmp(p->fault_stage, stage) != 0) return false;
+    p->fault_batch = -1;
+    return true;
+}
+
+void set_failed(asr_pipeline* p, long from, int rc) {
+    if (p->fail_from < 0 || from < p->fail_from) p->fail_from = from;
+    if (p->fail_rc == ASR_OK) p->fail_rc = rc;
+}
 
 int cu_stream(hipStream_t* s, int ncu, int lo, int hi) {
     static const int mask_all = [] { const char* e = getenv("ASR_PIPELINE_MASKALL"); return e ? atoi(e) : 0; }();
@@ -97,6 +120,7 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
     hipStream_t sp = p->s_prod[i % p->P];
+    if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
     asr_internal_rnn_kind = p->rnn_kind;
     int rc = asr_rnn_fwd(x, nullptr, p->W_ih, p->W_hh, p->b_ih, p->b_hh, p->hid[k], c.T, c.B, c.in, c.H, sp);
@@ -122,6 +146,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
     hipStream_t sp = p->s_prod[i % p->P];
     const long M = (long)c.T * c.B;
     const long ga = std::min(p->grows, M);
+    if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
     int rc = ASR_OK;
     if (ga > 0) {
@@ -152,6 +177,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
 int produce_head(asr_pipeline* p, long i, const float* x) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
+    if (fault(p, i, "head")) return ASR_ERR_INTERNAL;
     int rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], c.T * c.B, c.in, c.H, ASR_EPI_NONE, p->s_gemm);
     if (rc) return rc;
     ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gemm));
@@ -169,6 +195,7 @@ int produce_head(asr_pipeline* p, long i, const float* x) {
 int produce_tail(asr_pipeline* p, long i) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
+    if (fault(p, i, "tail")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_rec[k], 0));
     ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_free[k], 0));
     int rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
@@ -182,6 +209,7 @@ int enqueue_decode(asr_pipeline* p, long i) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
     hipStream_t sd = p->s_dec[i % p->D];
+    if (fault(p, i, "decode")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_ready[k], 0));
     int rc = asr_ctc_decode(p->dec[k], p->emis[k], c.T, c.B, 1, sd);
     if (rc) return rc;
@@ -200,6 +228,7 @@ int flush_tail(asr_pipeline* p) {
     int rc = produce_tail(p, j);
     const auto t1 = std::chrono::steady_clock::now();
     if (!rc) rc = enqueue_decode(p, j);
+    if (rc) set_failed(p, j, rc);   // batch j was accepted: its results can never come
     if (trace) {
         const auto t2 = std::chrono::steady_clock::now();
         const double a = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -214,10 +243,12 @@ int fetch(asr_pipeline* p, Result& r) {
     const auto& c = p->cfg;
     const long j = p->collected;
     if (j >= p->submitted) return ASR_ERR_STATE;
+    if (p->fail_from >= 0 && j >= p->fail_from) return p->fail_rc;
     if (j >= p->decoded) {
         int rc = flush_tail(p);
         if (rc) return rc;
     }
+    if (j >= p->decoded) return ASR_ERR_INTERNAL;   // never queued (cannot happen once flushed)
     asr_ctc_t* h = p->dec[j % p->nbuf];
     r.lab.assign((size_t)c.B * c.T, 0);
     r.len.assign(c.B, 0);
@@ -225,6 +256,7 @@ int fetch(asr_pipeline* p, Result& r) {
     r.rc = asr_ctc_get_best(h, r.lab.data(), c.T, r.len.data(), r.lp.data());
     if (r.rc != ASR_OK && r.rc != ASR_ERR_BEAM_OVERFLOW) return r.rc;
     asr_ctc_last_kernel_ms(h, &r.ms);
+    r.batch = j;
     p->collected = j + 1;
     return ASR_OK;
 }
@@ -260,6 +292,14 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         return ASR_ERR_ARG;
     asr_pipeline* p = new asr_pipeline();
     p->cfg = c;
+    if (const char* f = getenv("ASR_PIPELINE_FAULT")) {   // test hook: "<batch>:<stage>"
+        long b = -1;
+        char st[8] = {0};
+        if (sscanf(f, "%ld:%7s", &b, st) == 2) {
+            p->fault_batch = b;
+            std::memcpy(p->fault_stage, st, sizeof st);
+        }
+    }
     p->W_ih = W_ih; p->W_hh = W_hh; p->b_ih = b_ih; p->b_hh = b_hh; p->W_out = W_out; p->b_out = b_out;
     int dev = 0;
     int rc = ASR_OK;
@@ -347,6 +387,22 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         }
     }
     if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
+    // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
+    // hardware queues (default 4, read when the runtime starts), and streams
+    // that share a queue run one after another (C5, 5 streams on 4 queues:
+    // 1.03 M vs 3.48 M frames/s).  Fit the automatic schedule to the queues:
+    // fewer production streams first, then the decode CUs' share of the
+    // input projection, then fewer decodes in flight; explicit counts are
+    // kept as given.  asr_pipeline_get_streams reports the outcome.
+    {
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        p->hw_queues = (q && atoi(q) > 0) ? atoi(q) : 4;
+        auto nstreams = [&] { return p->D + p->P + (p->grows > 0 ? 1 : 0) + (p->split ? 1 : 0); };
+        while (nstreams() > p->hw_queues && !c.prod_streams && p->P > 1) p->P--;
+        if (nstreams() > p->hw_queues && p->grows > 0) p->grows = 0;
+        while (nstreams() > p->hw_queues && !c.inflight && p->D > 1) p->D--;
+        p->streams = nstreams();
+    }
     // D decoding + P producing (+1: split production queues the next input
     // projection before the previous batch's emission projection)
     p->nbuf = p->D + p->P + (p->split ? 1 : 0);
@@ -397,6 +453,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
 
 int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
     if (!p || !x) return ASR_ERR_ARG;
+    if (p->fail_rc) return p->fail_rc;
     const long i = p->submitted;
     // buffer i % nbuf is reused: its previous batch's results must be fetched first
     while (i - p->collected >= p->nbuf) {
@@ -416,19 +473,27 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
         last = now;
     };
     auto last = t0;
+    // A batch is accepted (counted as submitted) only once its production is
+    // queued; a failure before that returns the error and leaves the
+    // pipeline as it was (buffer i % nbuf is free: nothing else reads it).
+    // A failure in the rest of an accepted batch's work fails the pipeline
+    // from that batch on (set_failed): its results cannot come back.
     int rc;
     if (p->split) {
         rc = produce_head(p, i, x);
         if (trace) lap("head", last);
+        if (rc) return rc;
         p->submitted = i + 1;
-        if (!rc) rc = flush_tail(p);   // the previous batch: emission GEMM after this batch's input GEMM
+        rc = flush_tail(p);   // the previous batch: emission GEMM after this batch's input GEMM
         if (trace) lap("tail+decode", last);
         p->pending_tail = i;
     } else {
         rc = p->fuse ? produce_fused(p, i, x) : produce_full(p, i, x);
         if (trace) lap("produce", last);
+        if (rc) return rc;
         p->submitted = i + 1;
-        if (!rc) rc = enqueue_decode(p, i);
+        rc = enqueue_decode(p, i);
+        if (rc) set_failed(p, i, rc);
         if (trace) lap("decode", last);
     }
     return rc;
@@ -456,7 +521,17 @@ int asr_pipeline_collect(asr_pipeline_t* p, int32_t* labels, int max_len, int32_
         }
     }
     if (decode_ms) *decode_ms = r.ms;
+    p->returned = r.batch;
     return r.rc;
+}
+
+int asr_pipeline_peek_emissions(asr_pipeline_t* p, const float** d_emis) {
+    if (!p || !d_emis) return ASR_ERR_ARG;
+    *d_emis = nullptr;
+    // its buffer is rewritten by the production of batch returned + nbuf
+    if (p->returned < 0 || p->submitted - p->returned > p->nbuf) return ASR_ERR_STATE;
+    *d_emis = p->emis[p->returned % p->nbuf];
+    return ASR_OK;
 }
 
 int asr_pipeline_pending(asr_pipeline_t* p, int* n) {
@@ -482,10 +557,18 @@ int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod
     return ASR_OK;
 }
 
-int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows) {
+int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows, int* recurrence) {
     if (!p) return ASR_ERR_ARG;
     if (fused) *fused = p->fuse ? 1 : 0;
     if (decode_cu_rows) *decode_cu_rows = p->fuse ? p->grows : 0;
+    if (recurrence) *recurrence = p->rnn_kind >= 0 ? p->rnn_kind : ASR_RNN_RECUR_AUTO;
+    return ASR_OK;
+}
+
+int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues) {
+    if (!p) return ASR_ERR_ARG;
+    if (streams) *streams = p->streams;
+    if (hw_queues) *hw_queues = p->hw_queues;
     return ASR_OK;
 }
 

@@ -322,6 +322,12 @@ int asr_rnn_set_recurrence(int kind) {
     return ASR_OK;
 }
 
+int asr_rnn_get_recurrence(int* kind) {
+    if (!kind) return ASR_ERR_ARG;
+    *kind = g_rnn_recur_kind.load(std::memory_order_relaxed);
+    return ASR_OK;
+}
+
 int asr_rnn_fwd(const float* x, const float* h0, const float* W_ih, const float* W_hh,
                 const float* b_ih, const float* b_hh, float* hid, int T, int B, int in, int H,
                 asr_stream_t s) {

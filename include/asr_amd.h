@@ -129,9 +129,16 @@ int asr_rnn_recur_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_i
  *   but ~3x less CU time per utterance (for throughput pipelines whose
  *   production runs beside other work);
  * ASR_RNN_RECUR_AUTO (default) — MFMA from B >= 4 x CUs on.
- * Results agree to fp32 rounding (different summation order). */
+ * Results agree to fp32 rounding (different summation order), not bit for
+ * bit: under AUTO an utterance's hidden states therefore depend on the batch
+ * size it runs in (a batch of >= 4 x CUs and a smaller shard of it take
+ * different kernels).  Callers that need an utterance's bits to be
+ * independent of the batch (utterance sharding over GPUs, re-decoding a
+ * shard) pin a kind with asr_rnn_set_recurrence.  Thread-local overrides
+ * set by asr_pipeline_* never leak out of the pipeline's own calls. */
 enum { ASR_RNN_RECUR_AUTO = 0, ASR_RNN_RECUR_VALU = 1, ASR_RNN_RECUR_MFMA = 2 };
 int asr_rnn_set_recurrence(int kind);
+int asr_rnn_get_recurrence(int* kind);
 
 /* The recurrence and the emission layer in one pass — RNN::forward's
  * recurrence (RNN.cu:9-30) followed by Linear::forward (Linear.cu:42-49) with
@@ -281,7 +288,7 @@ int asr_ctc_get_config(asr_ctc_t* h, int* max_states, int* waves, int* lds_bytes
  * stream of equal-shape batches.  The library owns the streams, buffers and
  * decoder handles and overlaps the production of later batches with the
  * decodes of earlier ones, placing the kernels on the CUs for the shape
- * (DESIGN.md §7c).  Weights are caller-owned device arrays in the layouts of
+ * (DESIGN.md §7a-§7c).  Weights are caller-owned device arrays in the layouts of
  * asr_rnn_fwd / asr_linear_fwd and must outlive the pipeline. */
 typedef struct asr_pipeline asr_pipeline_t;
 typedef struct asr_pipeline_config {
@@ -300,7 +307,14 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* d_W_ih, con
  * batch's production, so it must stay unmodified until the batch is
  * collected).  Returns once the work is queued; when the caller is as many
  * batches behind as the pipeline has buffers, the oldest batch's results are
- * fetched internally first (asr_pipeline_collect still returns them). */
+ * fetched internally first (asr_pipeline_collect still returns them).
+ * Errors: a batch whose production could not be queued is not accepted (the
+ * error is returned and the pipeline is unchanged: submit it again or
+ * destroy).  If the rest of an accepted batch's work (this one's decode, or
+ * the previous batch's emission projection + decode in the split schedule)
+ * fails to queue, the pipeline is failed from that batch on: this and every
+ * later submit, and the collect of that batch and every later one, return
+ * the error; earlier batches are still collected normally. */
 int asr_pipeline_submit(asr_pipeline_t* p, const float* d_x);
 /* Results of the oldest uncollected batch, in submission order (blocks):
  * h_labels[B][max_len], h_lengths[B], h_logp[B] as asr_ctc_get_best, and the
@@ -320,9 +334,25 @@ int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod
  * NULL, P, ..., ASR_EPI_NONE) then asr_rnn_emit_fwd(NULL, W_hh, b_ih, b_hh,
  * W_out, b_out, P, NULL, emis, ...) gives its bits), 0 when it is
  * asr_rnn_fwd then asr_linear_fwd(..., ASR_EPI_BIAS_LOGSOFTMAX);
- * decode_cu_rows: input-projection rows run on the decode CUs.  Either
- * pointer may be NULL. */
-int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows);
+ * decode_cu_rows: input-projection rows run on the decode CUs; recurrence:
+ * the recurrence kind the unfused production pins (ASR_RNN_RECUR_*; AUTO =
+ * the process-wide choice), so a caller can reproduce the emissions bit for
+ * bit.  Any pointer may be NULL. */
+int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows, int* recurrence);
+/* Streams the pipeline created and the process's HIP hardware queues
+ * (GPU_MAX_HW_QUEUES as read at create; HIP's default is 4).  HIP maps
+ * streams round-robin onto the queues and streams that share a queue
+ * serialise, so the automatic schedule is fitted to the queues (fewer
+ * production streams, then no input-projection share on the decode CUs,
+ * then fewer decodes in flight); streams > hw_queues only when the caller
+ * fixed inflight / prod_streams.  DESIGN.md §7c gives the measured cost. */
+int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues);
+/* The emissions [T][B][V] (log-probabilities, device) that the decode of the
+ * batch last returned by asr_pipeline_collect consumed — the exact bytes, for
+ * parity checks of the pipelined path.  Valid until the next submit that
+ * reuses the buffer; ASR_ERR_STATE if nothing was collected yet or the
+ * buffer has been reused. */
+int asr_pipeline_peek_emissions(asr_pipeline_t* p, const float** d_emis);
 int asr_pipeline_destroy(asr_pipeline_t* p);
 
 #ifdef __cplusplus

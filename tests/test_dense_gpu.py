@@ -115,6 +115,29 @@ def test_linear_wide_persistent(M, K, N, epi, monkeypatch):
     assert np.array_equal(y2.toCpu(), got)
 
 
+@pytest.mark.parametrize("K", [64, 100, 128])
+def test_linear_wide_after_lds_poison(K):
+    """The persistent wide GEMM (M >= 131072, N >= 128, K <= 256) after a
+    kernel that left every CU's LDS full of 0xFFFFFFFF (NaN as fp32): the
+    B^T slice past K must be zero-filled, not read as left over (ADVICE r3
+    #1; the MFMA loop runs all 256 / 16 chunks)."""
+    import ctypes
+    from conftest import ROOT
+    helper = ctypes.CDLL(str(ROOT / "tests" / "helpers" / "liblds_poison.so"))
+    helper.lds_poison.argtypes = [ctypes.c_void_p]
+    M, N = 131072, 128
+    rng = np.random.default_rng(K)
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = rng.uniform(-1, 1, (K, N)).astype(np.float32)
+    dx, dW, dy = dm(x), dm(W), asr.DeviceMatrix(M, N)
+    asr.synchronize()
+    assert helper.lds_poison(None) == 0
+    asr.linear_fwd(dx, dW, None, dy, asr.EPI_NONE)
+    y = dy.toCpu()
+    assert np.all(np.isfinite(y)), "NaN from stale LDS"
+    close(y, (torch.from_numpy(x) @ torch.from_numpy(W)).numpy())
+
+
 @pytest.mark.parametrize("M,K,N", [(32000, 256, 29), (100, 64, 5), (77, 30, 64), (300, 1024, 1000), (9, 16, 65)])
 def test_linear_logsoftmax(M, K, N):
     rng = np.random.default_rng(N)

@@ -123,3 +123,61 @@ def test_pipeline_input_projection_on_decode_cus(gsplit, monkeypatch):
     for g, x in zip(got, xs):
         ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
         assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+
+
+@pytest.mark.parametrize("B,stage", [(16, "head"), (16, "tail"), (300, "produce"), (300, "decode")])
+def test_pipeline_failure_is_reported(B, stage, monkeypatch):
+    """A batch whose production cannot be queued is not accepted (the error
+    comes back, the pipeline is unchanged); a failure in an accepted batch's
+    later work fails the pipeline from that batch on — its collect and every
+    later call return the error, never another batch's stale results — while
+    earlier batches are still collected normally.  The
+    library's test hook ASR_PIPELINE_FAULT=<batch>:<stage> fails one stage
+    of one batch once."""
+    T, inp, H, V, beam = 20, 32, 64, 29, 10
+    monkeypatch.setenv("ASR_PIPELINE_FAULT", f"2:{stage}")
+    W = _weights(inp, H, V, seed=5)
+    rng = np.random.default_rng(9)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(5)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert (d["mode"] == "CU groups (small batches)") == (B == 16), d
+
+    def ref(x):
+        return _sequential(x, W, T, B, inp, H, V, beam, d["recurrence"], d["fused_emission"])
+
+    def take():
+        lab, ln, lp, _ = p.collect()
+        return [lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()
+
+    p.submit(xs[0])
+    p.submit(xs[1])
+    if stage in ("head", "produce"):   # batch 2 is refused, nothing else changes
+        with pytest.raises(asr.AsrError) as ei:
+            p.submit(xs[2])
+        assert ei.value.status == asr.ASR_ERR_INTERNAL
+        assert p.pending() == 2
+        p.submit(xs[3])   # accepted as batch 2
+        got = [take() for _ in range(3)]
+        for g, x in zip(got, (xs[0], xs[1], xs[3])):
+            r = ref(x)
+            assert g[0] == r[0] and np.array_equal(g[1], r[1])
+    else:
+        # tail: batch 2's emission GEMM + decode are queued by the submit of
+        # batch 3 (split schedule); decode: by batch 2's own submit
+        if stage == "tail":
+            p.submit(xs[2])
+            with pytest.raises(asr.AsrError):
+                p.submit(xs[3])
+        else:
+            with pytest.raises(asr.AsrError):
+                p.submit(xs[2])
+        for i in range(2):   # batches 0 and 1 were fine
+            g, r = take(), ref(xs[i])
+            assert g[0] == r[0] and np.array_equal(g[1], r[1])
+        with pytest.raises(asr.AsrError) as ei:   # batch 2: the error, not stale results
+            p.collect()
+        assert ei.value.status == asr.ASR_ERR_INTERNAL
+        with pytest.raises(asr.AsrError):
+            p.submit(xs[4])
+    p.close()

@@ -5,6 +5,8 @@
 #   trace  kernel trace + stats
 #   fetch  FETCH_SIZE            write  WRITE_SIZE
 #   sq     8 SQ issue counters   grbm   GRBM_GUI_ACTIVE GRBM_COUNT
+#   valu   VALU mix (fp64)       mfma   MFMA busy / instruction counters + GRBM
+#   list   rocprofv3 -L (the counters this box offers)
 # Stops at the first failing pass.  Summaries are made on the dev side:
 #   tools/traffic_from_pmc.py, tools/issue_from_pmc.py -> profiles/<round>/
 #
@@ -16,6 +18,10 @@ OUT=gpurun_out/prof_${OUT:-run}
 mkdir -p "$OUT"
 ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+# the decoder's VALU mix (fp64 share, VALU issue cycles) and the scalar unit
+VALU="SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES"
+# matrix-core evidence of the dense kernels (+ the clock)
+MFMA="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
 for pass in ${PASSES:-trace fetch write}; do
     case $pass in
         trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
@@ -26,6 +32,11 @@ for pass in ${PASSES:-trace fetch write}; do
                    -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 ;;
         sq)    timeout -s KILL 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/sq" -o run \
                    -- python3 bench.py $ARGS > "$OUT/sq.log" 2>&1 ;;
+        list)  timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_avail.txt" 2>&1 ;;
+        valu)  timeout -s KILL 180 rocprofv3 --pmc $VALU --output-format csv -d "$OUT/valu" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/valu.log" 2>&1 ;;
+        mfma)  timeout -s KILL 180 rocprofv3 --pmc $MFMA --output-format csv -d "$OUT/mfma" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/mfma.log" 2>&1 ;;
         grbm)  timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/grbm" -o run \
                    -- python3 bench.py $ARGS > "$OUT/grbm.log" 2>&1 ;;
         *) echo "unknown pass $pass"; exit 2 ;;
