@@ -20,6 +20,7 @@ struct CtcGeom {
     int ch;      // emission frames staged per prefetch chunk
     int ht;      // orphan-table cells (4 x row capacity, 8-cell buckets)
     int lbits;   // bits per label in node records and tails: 8 (V <= 64) or 16
+    int ts;      // timesteps mode: the workgroup kernel's TS0/TS1 arrays are allocated (Lds::total_ts)
 };
 
 struct CtcArgs {

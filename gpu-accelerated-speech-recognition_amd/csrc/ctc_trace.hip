@@ -9,9 +9,9 @@ int ctc_row_capacity(int kcap) { return kcap <= 64 ? 64 : (kcap <= 128 ? 128 : 2
 size_t ctc_lds_bytes(const CtcGeom& g) {
     if (g.V + 1 > 64) return ctc_lds_bytes_wide(ctc_row_capacity(g.kcap), g.V);
     switch (ctc_row_capacity(g.kcap)) {
-    case 64: return Lds<64>::total(g.ch, g.V);
-    case 128: return Lds<128>::total(g.ch, g.V);
-    default: return Lds<256>::total(g.ch, g.V);
+    case 64: return g.ts ? Lds<64>::total_ts(g.ch, g.V) : Lds<64>::total(g.ch, g.V);
+    case 128: return g.ts ? Lds<128>::total_ts(g.ch, g.V) : Lds<128>::total(g.ch, g.V);
+    default: return g.ts ? Lds<256>::total_ts(g.ch, g.V) : Lds<256>::total(g.ch, g.V);
     }
 }
 

@@ -547,6 +547,7 @@ asr::CtcGeom plan(const asr_ctc* h, int waves) {
     (void)waves;
     g.ch = std::max(1, std::min(32, 1024 / h->V));   // chunk = ch*V <= 1024 emissions (16 per thread at 1 wave)
     g.ht = 4 * asr::ctc_row_capacity(h->kcap);
+    g.ts = h->ts ? 1 : 0;
     return g;
 }
 
@@ -712,8 +713,15 @@ int asr_ctc_set_result_stream(asr_ctc_t* h, asr_stream_t s) {
 
 int asr_ctc_set_timesteps(asr_ctc_t* h, int on) {
     if (!h) return ASR_ERR_ARG;
+    const int prev = h->ts;
     h->ts = on ? 1 : 0;
+    // the workgroup kernel's timestep arrays are allocated only in this mode
+    if (h->ts && h->V + 1 <= 64 && asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) {
+        h->ts = prev;
+        return ASR_ERR_UNSUPPORTED;
+    }
     if (h->wide) h->wide->ts = h->ts;
+    if (h->ts != prev) h->occ8 = h->occ4 = -1;   // the layout changed: re-query the occupancy
     h->have = false;
     return ASR_OK;
 }
