@@ -53,12 +53,12 @@ EXPORTS = [
     "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_recur_fwd", "asr_rnn_emit_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
     "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
-    "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_set_semantics",
+    "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_decode_segment", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
     "asr_ctc_set_concurrency", "asr_rnn_set_recurrence", "asr_rnn_get_recurrence",
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
     "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams",
-    "asr_pipeline_peek_emissions",
+    "asr_pipeline_peek_emissions", "asr_pipeline_get_segments",
     "asr_pipeline_destroy",
 ]
 
@@ -126,6 +126,7 @@ def lib() -> ctypes.CDLL:
                                         ctypes.POINTER(_i)],
         "asr_pipeline_get_streams": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_pipeline_peek_emissions": [_vp, ctypes.POINTER(_vp)],
+        "asr_pipeline_get_segments": [_vp, ctypes.POINTER(_i)],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -137,6 +138,7 @@ def lib() -> ctypes.CDLL:
         "asr_ctc_set_concurrency": [_vp, _i],
         "asr_ctc_get_config": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_ctc_decode_ex": [_vp, _vp, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
+        "asr_ctc_decode_segment": [_vp, _vp, _i, _i, _i, _i, ctypes.c_long, ctypes.c_long, _vp, _i, _vp],
         "asr_ctc_set_semantics": [_vp, _i],
         "asr_ctc_set_timesteps": [_vp, _i],
         "asr_ctc_set_result_stream": [_vp, _vp],
@@ -432,6 +434,23 @@ class CTCDecoder:
               "asr_ctc_decode_ex")
         self.T, self.B = T, B
 
+    def decode_segment(self, d_emis: int, T: int, t0: int, t1: int, B: int, is_log: bool, stream: int = 0,
+                       lengths: Optional[Sequence[int]] = None, frame_stride: Optional[int] = None,
+                       utt_stride: Optional[int] = None) -> None:
+        """Frames [t0, t1) of a T-frame batch (asr_ctc_decode_segment): d_emis
+        addresses frame t0 (element (t, b, v) at d_emis + ((t - t0)*frame_stride
+        + b*utt_stride + v) floats); segments in order from 0 to T, then
+        best() / beams() as after decode_device."""
+        fs = B * self.V if frame_stride is None else int(frame_stride)
+        us = self.V if utt_stride is None else int(utt_stride)
+        ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.int32)
+        if ln is not None:
+            assert ln.shape == (B,), (ln.shape, B)
+        check(lib().asr_ctc_decode_segment(self.h, d_emis, T, t0, t1, B, fs, us,
+                                           _ptr(ln) if ln is not None else None, int(bool(is_log)), stream),
+              "asr_ctc_decode_segment")
+        self.T, self.B = T, B
+
     def decode(self, emis: np.ndarray, is_log: bool = False, stream: int = 0,
                lengths: Optional[Sequence[int]] = None, batch_major: bool = False) -> None:
         """Upload emissions (fp32 [T][B][V], or [B][T][V] with batch_major) and
@@ -514,7 +533,7 @@ class CTCDecoder:
 class PipelineConfig(ctypes.Structure):
     """asr_pipeline_config (include/asr_amd.h)."""
     _fields_ = [(n, ctypes.c_int) for n in ("T", "B", "in_", "H", "V", "beam", "blank", "inflight",
-                                           "prod_streams", "decode_cus")]
+                                           "prod_streams", "decode_cus", "segments")]
 
 
 PIPELINE_MODES = {0: "CU groups (small batches)", 1: "chip-filling batches", 2: "CU groups (H > 256)"}
@@ -558,9 +577,9 @@ class Pipeline:
     (labels [B][T], lengths [B], logp [B], decode_ms)."""
 
     def __init__(self, T: int, B: int, inp: int, H: int, V: int, beam: int, weights, blank: int = 0,
-                 inflight: int = 0, prod_streams: int = 0, decode_cus: int = 0):
+                 inflight: int = 0, prod_streams: int = 0, decode_cus: int = 0, segments: int = 0):
         self.T, self.B = T, B
-        self.cfg = PipelineConfig(T, B, inp, H, V, beam, blank, inflight, prod_streams, decode_cus)
+        self.cfg = PipelineConfig(T, B, inp, H, V, beam, blank, inflight, prod_streams, decode_cus, segments)
         self._w = weights   # (W_ih, W_hh, b_ih, b_hh, W_out, b_out) DeviceMatrix: kept alive
         h = _vp()
         check(lib().asr_pipeline_create(ctypes.byref(self.cfg), *[w.ptr for w in weights], ctypes.byref(h)),
@@ -579,12 +598,13 @@ class Pipeline:
         fz, gr, rk = _i(), ctypes.c_longlong(), _i()
         check(lib().asr_pipeline_get_production(self.h, ctypes.byref(fz), ctypes.byref(gr), ctypes.byref(rk)),
               "asr_pipeline_get_production")
-        ns, hq = _i(), _i()
+        ns, hq, sg = _i(), _i(), _i()
         check(lib().asr_pipeline_get_streams(self.h, ctypes.byref(ns), ctypes.byref(hq)), "asr_pipeline_get_streams")
+        check(lib().asr_pipeline_get_segments(self.h, ctypes.byref(sg)), "asr_pipeline_get_segments")
         return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
                 "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
                 "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
-                "hw_queues": hq.value}
+                "hw_queues": hq.value, "segments": sg.value}
 
     def submit(self, x: "DeviceMatrix") -> None:
         """Queue a batch.  x is kept alive here until its batch is collected

@@ -36,6 +36,11 @@ extern thread_local int asr_internal_rnn_kind;
 // kernel (short-lived workgroups) instead of the persistent wide one, so that
 // a decode launched meanwhile waits at most one tile for its CUs.  Same bits.
 extern thread_local int asr_internal_gemm_tiled;
+// One-wave decoder workgroups (utterances) that fit on one CU for this
+// handle's layout (the occupancy query); 0 when the one-wave kernel does not
+// apply (V > 63, .cu semantics, timesteps).  For the pipeline's schedule.
+struct asr_ctc;
+int asr_internal_ctc_wave_occupancy(asr_ctc* h);
 
 // Order-preserving bijection fp64 <-> u64: a < b  <=>  key(a) < key(b).
 // -0.0 is folded onto +0.0 (they compare equal as doubles).  Key 0 is never

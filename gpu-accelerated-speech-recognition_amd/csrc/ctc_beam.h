@@ -47,6 +47,14 @@ struct CtcArgs {
     uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
     uint32_t* tile0;        // [B][T][WREC] first label tile per frame (wide kernel, V > 65; NULL: in-kernel)
     int diag;               // bit 0: the wide kernel always takes its register fallback (tests; ASR_CTC_WIDE_FALLBACK=1)
+    // Segmented decode (asr_ctc_decode_segment; one-wave kernel only): this
+    // launch runs frames [t0, t1) of T, emis addresses frame t0, and the beam
+    // of every unfinished utterance is saved to / restored from seg_state
+    // [B][seg_bytes] at the segment ends.  A whole decode: t0 = 0, t1 = T,
+    // seg_state = NULL.
+    int t0, t1;
+    unsigned char* seg_state;
+    int seg_bytes;
 };
 
 int ctc_row_capacity(int kcap);   // compile-time slot capacity KC >= kcap (64, 128, 256)
@@ -73,6 +81,7 @@ size_t ctc_lds_bytes_wave(const CtcGeom& g);
 bool ctc_wave_supported(const CtcGeom& g, int cu_mode);
 int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s);
 int ctc_occupancy_wave(const CtcGeom& g);   // one-wave workgroups per CU
+size_t ctc_seg_bytes_wave(const CtcGeom& g);  // saved beam per utterance between segments
 int ctc_set_max_lds_wave();
 // waves < 0: the one-wave list kernel; 1..8: the workgroup kernel with that many waves.
 int ctc_launch_decode(const CtcArgs& a, int waves, hipStream_t s);

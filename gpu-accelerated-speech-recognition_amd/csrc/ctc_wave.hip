@@ -13,6 +13,15 @@ size_t ctc_lds_bytes_wave(const CtcGeom& g) {
     }
 }
 
+size_t ctc_seg_bytes_wave(const CtcGeom& g) {
+    const bool c64 = g.V > 32;
+    switch (ctc_row_capacity(g.kcap)) {
+    case 64: return c64 ? WLds<64, true>::SEG : WLds<64, false>::SEG;
+    case 128: return c64 ? WLds<128, true>::SEG : WLds<128, false>::SEG;
+    default: return c64 ? WLds<256, true>::SEG : WLds<256, false>::SEG;
+    }
+}
+
 bool ctc_wave_supported(const CtcGeom& g, int cu_mode) {
     return !cu_mode && g.V + 1 <= 64 && g.kcap <= 256 && ctc_lds_bytes_wave(g) <= 160u * 1024u;
 }

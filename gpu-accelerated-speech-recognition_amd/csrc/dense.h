@@ -33,10 +33,11 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
 int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                           float* hid, int T, int B, int H, hipStream_t s);
 // The MFMA recurrence with the emission projection + log_softmax fused
-// (V <= 32): P [T][B][H] read only, hidden states to hout (NULL: not stored).
+// (V <= 32): P [T][B][H] read only, hidden states to hout (NULL: not stored);
+// hlast [B][H] (optional, may be h0): h_{T-1}, the h0 of a next segment.
 int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                          const float* P, float* hout, const float* Wout, const float* bout, float* emis,
-                         int T, int B, int H, int V, hipStream_t s);
+                         int T, int B, int H, int V, hipStream_t s, float* hlast = nullptr);
 int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
 int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
 int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);

@@ -661,7 +661,7 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
                                                              const float* __restrict__ Wout,
                                                              const float* __restrict__ bout,
                                                              float* __restrict__ emis, int T, int B,
-                                                             int H, int V) {
+                                                             int H, int V, float* hlast) {
     __shared__ __attribute__((aligned(16))) float hs[2][RM_ROWS * RM_LD];
     __shared__ __attribute__((aligned(16))) float ep[EMIT ? 2 : 1][EMIT ? RE_PART : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -864,6 +864,12 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
         cur ^= 1;
         lds_barrier();
     }
+    if (hlast) {   // h_{T-1} of this workgroup's rows (may be h0's buffer: every row is read above)
+        for (int x = tid; x < RM_ROWS * H; x += nthr) {
+            const int r = x / H, k = x - r * H;
+            if (r0 + r < B) hlast[(long)(r0 + r) * H + k] = hs[cur][r * RM_LD + k];
+        }
+    }
     if (EMIT) {   // the last two frames' emissions
         f32x4 ea[2];
         emit_partial(cur, ea);   // h_{T-1}
@@ -880,19 +886,19 @@ int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, 
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
     hipLaunchKernelGGL(rnn_recur_mfma_kernel<false>, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
                        dim3(64 * ((H / 16 + 1) / 2)), 0, s,
-                       h0, Whh, b_ih, b_hh, hid, nullptr, nullptr, nullptr, nullptr, T, B, H, 0);
+                       h0, Whh, b_ih, b_hh, hid, nullptr, nullptr, nullptr, nullptr, T, B, H, 0, nullptr);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }
 
 int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                          const float* P, float* hout, const float* Wout, const float* bout, float* emis,
-                         int T, int B, int H, int V, hipStream_t s) {
+                         int T, int B, int H, int V, hipStream_t s, float* hlast) {
     if (H > RNN_HMAX || (H & 15) != 0 || B <= 0 || V < 1 || V > RE_VMAX) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
     hipLaunchKernelGGL(rnn_recur_mfma_kernel<true>, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
                        dim3(64 * ((H / 16 + 1) / 2)), 0, s,
-                       h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H, V);
+                       h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H, V, hlast);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "asr_internal.h"
+#include "dense.h"
 
 namespace {
 
@@ -67,6 +68,9 @@ struct asr_pipeline {
     bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
     bool gtiled = false;  // ... with the tiled GEMM kernel (several decodes in flight)
+    int S = 1;            // T-segments per batch (fused production only)
+    std::vector<float*> hst;          // [nbuf][B][H] the recurrence's h at a segment end
+    std::vector<hipEvent_t> ev_seg;   // [nbuf][S] segment s of buffer k's emissions ready
     hipStream_t s_gdec = nullptr;   // the decode CUs' share of the input projections
     std::vector<float*> hid, emis;
     std::vector<asr_ctc_t*> dec;
@@ -95,6 +99,16 @@ bool fault(asr_pipeline* p, long i, const char* stage) {   // fires once
     if (i != p->fault_batch || std::strcmp(p->fault_stage, stage) != 0) return false;
     p->fault_batch = -1;
     return true;
+}
+
+// One-wave decoder utterances per CU for this configuration's beam (0: the
+// one-wave kernel does not apply).
+int wave_occupancy(const asr_pipeline_config& c) {
+    asr_ctc_t* h = nullptr;
+    if (asr_ctc_create(nullptr, c.V, c.beam, c.blank, 0, &h) != ASR_OK) return 0;
+    const int n = asr_internal_ctc_wave_occupancy(h);
+    asr_ctc_destroy(h);
+    return n;
 }
 
 void set_failed(asr_pipeline* p, long from, int rc) {
@@ -132,6 +146,46 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     return ASR_OK;
 }
 
+// The fused production in S T-segments: segment s (frames [t0, t1)) is its
+// rows of the input projection (the decode CUs' share first, as below), then
+// the fused recurrence over those frames from h_{t0-1} (hst[k], written by
+// segment s-1), its last h to hst[k]; event ev_seg[k][s] releases the
+// decode of those frames.  The same kernels over the same rows in the same
+// order: the emissions are the unsegmented production's bits.
+int produce_fused_segments(asr_pipeline* p, long i, const float* x, hipStream_t sp) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    const long frac128 = p->grows;   // decode-CU rows of the whole batch
+    int rc = ASR_OK;
+    if (frac128 > 0) ASR_HIP_TRY(hipStreamWaitEvent(p->s_gdec, p->ev_free[k], 0));
+    for (int s = 0; s < p->S && !rc; s++) {
+        const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
+        const long r0 = (long)t0 * c.B, rows = (long)(t1 - t0) * c.B;
+        const long ga = frac128 > 0 ? std::min(rows, frac128 * rows / ((long)c.T * c.B) / 128 * 128) : 0;
+        if (ga > 0) {
+            asr_internal_gemm_tiled = p->gtiled ? 1 : 0;
+            rc = asr_linear_fwd(x + r0 * c.in, p->W_ih, nullptr, p->hid[k] + r0 * c.H, (int)ga, c.in, c.H,
+                                ASR_EPI_NONE, p->s_gdec);
+            asr_internal_gemm_tiled = 0;
+            if (rc) return rc;
+            ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
+        }
+        if (ga < rows)
+            rc = asr_linear_fwd(x + (r0 + ga) * c.in, p->W_ih, nullptr, p->hid[k] + (r0 + ga) * c.H, (int)(rows - ga),
+                                c.in, c.H, ASR_EPI_NONE, sp);
+        if (rc) return rc;
+        if (ga > 0) ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_proj[k], 0));
+        rc = asr::rnn_emit_mfma_launch(s > 0 ? p->hst[k] : nullptr, p->W_hh, p->b_ih, p->b_hh,
+                                       p->hid[k] + r0 * c.H, nullptr, p->W_out, p->b_out,
+                                       p->emis[k] + (long)t0 * c.B * c.V, t1 - t0, c.B, c.H, c.V, sp,
+                                       s + 1 < p->S ? p->hst[k] : nullptr);
+        if (rc) return rc;
+        ASR_HIP_TRY(hipEventRecord(p->ev_seg[(size_t)k * p->S + s], sp));
+    }
+    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
+    return ASR_OK;
+}
+
 // Fused production of batch i into buffer k (chip-filling batches, H <= 256,
 // V <= 32): the input projection P = x.W_ih into hid[k] — its first grows rows
 // on the decode CUs (s_gdec, which runs them whenever the decodes leave those
@@ -148,6 +202,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
     const long ga = std::min(p->grows, M);
     if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    if (p->S > 1) return produce_fused_segments(p, i, x, sp);
     int rc = ASR_OK;
     if (ga > 0) {
         ASR_HIP_TRY(hipStreamWaitEvent(p->s_gdec, p->ev_free[k], 0));
@@ -210,8 +265,18 @@ int enqueue_decode(asr_pipeline* p, long i) {
     const int k = (int)(i % p->nbuf);
     hipStream_t sd = p->s_dec[i % p->D];
     if (fault(p, i, "decode")) return ASR_ERR_INTERNAL;
-    ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_ready[k], 0));
-    int rc = asr_ctc_decode(p->dec[k], p->emis[k], c.T, c.B, 1, sd);
+    int rc = ASR_OK;
+    if (p->S > 1) {   // segment by segment, each behind its production
+        for (int s = 0; s < p->S && !rc; s++) {
+            const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
+            ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_seg[(size_t)k * p->S + s], 0));
+            rc = asr_ctc_decode_segment(p->dec[k], p->emis[k] + (long)t0 * c.B * c.V, c.T, t0, t1, c.B,
+                                        (long)c.B * c.V, c.V, nullptr, 1, sd);
+        }
+    } else {
+        ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_ready[k], 0));
+        rc = asr_ctc_decode(p->dec[k], p->emis[k], c.T, c.B, 1, sd);
+    }
     if (rc) return rc;
     ASR_HIP_TRY(hipEventRecord(p->ev_free[k], sd));
     p->decoded = i + 1;
@@ -269,6 +334,8 @@ void release(asr_pipeline* p) {
     for (auto h : p->dec) asr_ctc_destroy(h);
     for (auto b : p->hid) hipFree(b);
     for (auto b : p->emis) hipFree(b);
+    for (auto b : p->hst) hipFree(b);
+    for (auto e : p->ev_seg) if (e) hipEventDestroy(e);
     for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec})
         for (auto e : *v) if (e) hipEventDestroy(e);
     for (auto s : p->s_dec) if (s) hipStreamDestroy(s);
@@ -288,7 +355,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     *out = nullptr;
     const auto& c = *cfg;
     if (c.T < 1 || c.B < 1 || c.in < 1 || c.H < 1 || c.V < 2 || c.beam < 1 || c.blank < 0 || c.blank >= c.V ||
-        c.inflight < 0 || c.prod_streams < 0 || c.decode_cus < -1)
+        c.inflight < 0 || c.prod_streams < 0 || c.decode_cus < -1 || c.segments < 0)
         return ASR_ERR_ARG;
     asr_pipeline* p = new asr_pipeline();
     p->cfg = c;
@@ -313,13 +380,15 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     const int K = c.beam + 1;
     const int kcap = (K + std::max(8, K / 8) + 31) / 32 * 32;
     const int bcu = (c.B + 7) / 8 * 8;   // CUs at one decode workgroup per utterance
+    int occw = 0;                          // one-wave decoder workgroups per CU (SHARED)
     if (c.H <= 256 && c.V + 1 <= 64 && 4 * bcu <= ncu) {
         p->mode = GROUPS;
         p->gcu = bcu;
         p->D = c.inflight ? c.inflight : std::max(1, std::min(3, ncu / bcu - 1));
         p->P = 1;
         p->split = true;
-    } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 64 && 2 * bcu > ncu) {
+    } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 128 && 2 * bcu > ncu &&
+               (occw = wave_occupancy(c)) > 0) {
         p->mode = SHARED;
         p->rnn_kind = ASR_RNN_RECUR_MFMA;
         // decodes and production on their own halves of the CUs (the
@@ -335,11 +404,16 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // whose production costs more CU time per frame (the input GEMM of a
         // short M; measured at 256 per GPU, 60 steps: 128 / 96 / 80 decode
         // CUs 137-142 / 155-162 / 145 M frames/s; at 512: 128 / 96 CUs
-        // 183 / 168-182 M; profiles/r03/bench_scan.md)
-        const int dauto = (c.B < 512 ? ncu * 3 / 8 : ncu / 2) / 8 * 8;
+        // 183 / 168-182 M; profiles/r03/bench_scan.md).  Beam capacity
+        // 65-128 (C3's beam 100: two rows per lane): an utterance-frame costs
+        // the decoder ~4x the CU time (0.49 vs 2.0 utterance-frames per us
+        // per CU), the production the same, so 3/4 of the CUs decode.
+        const int dauto = (kcap > 64 ? ncu * 3 / 4 : (c.B < 512 ? ncu * 3 / 8 : ncu / 2)) / 8 * 8;
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : dauto) : 0;
         const int dc = p->dcus ? p->dcus : ncu;
-        const int Dw = std::max(1, std::min(8, (16 * dc + c.B / 2) / c.B));   // 16 decodes per CU
+        // as many batches decoding at once as fill the decode CUs at the
+        // one-wave kernel's occupancy (16 per CU at beam <= 56, ~9 at 100)
+        const int Dw = std::max(1, std::min(8, (occw * dc + c.B / 2) / c.B));
         p->D = c.inflight ? c.inflight : Dw;
         // production streams: the recurrence of a batch is latency-bound
         // (T steps) on B / 16 CUs, so as many batches produce at once as
@@ -360,7 +434,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             // CUs (1024 per GPU: 171 vs 180 M at 0.3 / 0), with the tiled one
             // 0 / 0.2 / 0.3 -> 173 / 196 / 198 M, 512 per GPU 167 / 182 / 182 M
             // (profiles/r03/bench_scan.md)
-            const double f = ge ? atof(ge) : 0.3;
+            // two rows per lane: the decode CUs are the busier half, no share (A/B)
+            const double f = ge ? atof(ge) : (kcap > 64 ? 0.0 : 0.3);
             p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
             const char* gt = getenv("ASR_PIPELINE_GTILED");   // A/B: 1 / 0 force, default: D > 1
             p->gtiled = gt ? atoi(gt) != 0 : p->D > 1;
@@ -387,6 +462,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         }
     }
     if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
+    // T-segments (fused production only): explicit, ASR_PIPELINE_SEGMENTS
+    // (A/B), else 1
+    if (p->fuse && p->mode == SHARED) {
+        const char* se = getenv("ASR_PIPELINE_SEGMENTS");
+        int S = c.segments ? c.segments : (se ? atoi(se) : 1);
+        p->S = std::max(1, std::min(S, c.T));
+    }
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
     // hardware queues (default 4, read when the runtime starts), and streams
     // that share a queue run one after another (C5, 5 streams on 4 queues:
@@ -432,10 +514,22 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         asr_ctc_t* h = nullptr;
         if (!rc) rc = asr_ctc_create(nullptr, c.V, c.beam, c.blank, 0, &h);
         p->dec.push_back(h);
+        if (p->S > 1) {
+            float* hs = nullptr;
+            if (!rc && hipMalloc(&hs, sizeof(float) * (size_t)c.B * c.H) != hipSuccess) rc = ASR_ERR_OOM;
+            p->hst.push_back(hs);
+            for (int s = 0; s < p->S; s++) {
+                hipEvent_t e = nullptr;
+                if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;
+                p->ev_seg.push_back(e);
+            }
+        }
         // the decoders' schedule (asr_ctc_set_concurrency): D batches share the
         // decode CUs, which are dcus of the ncu the decoder plans for
         const int conc = p->mode == SHARED ? (p->D * ncu + (p->dcus ? p->dcus : ncu) - 1) / (p->dcus ? p->dcus : ncu) : 1;
         if (!rc && conc > 1) rc = asr_ctc_set_concurrency(h, conc);
+        // chip-filling batches: many utterances per decode CU, the one-wave kernel
+        if (!rc && p->mode == SHARED && occw > 0) rc = asr_ctc_set_waves(h, ASR_CTC_WAVES_LIST);
         for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec}) {
             hipEvent_t e = nullptr;
             if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;
@@ -562,6 +656,12 @@ int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode
     if (fused) *fused = p->fuse ? 1 : 0;
     if (decode_cu_rows) *decode_cu_rows = p->fuse ? p->grows : 0;
     if (recurrence) *recurrence = p->rnn_kind >= 0 ? p->rnn_kind : ASR_RNN_RECUR_AUTO;
+    return ASR_OK;
+}
+
+int asr_pipeline_get_segments(asr_pipeline_t* p, int* segments) {
+    if (!p || !segments) return ASR_ERR_ARG;
+    *segments = p->S;
     return ASR_OK;
 }
 

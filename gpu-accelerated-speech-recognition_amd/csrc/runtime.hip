@@ -476,6 +476,14 @@ struct asr_ctc {
     int* d_lengths = nullptr;        // per-utterance frames (asr_ctc_decode_ex)
     int* h_lengths = nullptr;        // pinned staging
     int cap_len = 0;
+    // segmented decode (asr_ctc_decode_segment)
+    int seg_next = 0;                // first frame of the next segment (0: none in progress)
+    int seg_T = 0, seg_B = 0, seg_is_log = 0;
+    long seg_fs = 0, seg_us = 0;
+    unsigned char* d_seg = nullptr;  // [B][seg_bytes] saved beams
+    size_t cap_seg = 0;
+    std::vector<hipEvent_t> seg_ev;  // (start, end) of each segment's kernel, for last_kernel_ms
+    int nseg = 0;                    // segments of the current / last segmented decode
 };
 
 namespace {
@@ -508,13 +516,21 @@ double rel_4w(int n) { return n <= 3 ? REL_4W[n] : REL_4W[3] * n / 3.0; }
 // utterances per CU on it decodes a batch fastest.
 constexpr double REL_W[17] = {0.0,  1.84, 1.89, 1.96, 2.23, 2.39, 2.54, 2.55, 2.55,
                               2.65, 2.74, 2.84, 2.94, 3.08, 3.22, 3.36, 3.50};
-double rel_w(int n) { return n <= 16 ? REL_W[n] : REL_W[16] * n / 16.0; }
+// Two rows per lane (beam capacity 65-128, C3's beam 100): against the
+// 8-wave kernel alone (4.79 us per frame), 2.69 / 2.82 / 2.88 / 3.43 at 1 / 2
+// / 4 / 8 per CU (tools/occupancy_sweep.py --beam 100, profiles/r04/), a CU
+// holding ~9 (LDS); between the points linear.
+constexpr double REL_W2[10] = {0.0, 2.69, 2.82, 2.85, 2.88, 3.02, 3.16, 3.29, 3.43, 3.57};
+double rel_w(int n, int kcap) {
+    if (kcap > 64) return n <= 9 ? REL_W2[n] : REL_W2[9] * n / 9.0;
+    return n <= 16 ? REL_W[n] : REL_W[16] * n / 16.0;
+}
 int auto_waves(asr_ctc* h, int B) {
     if (h->cu_mode || h->V + 1 > 64 || h->V + 1 <= 8 || B <= 0) return 8;
     if (h->occ8 < 0) {   // once per handle: the layout is fixed at creation
         h->occ8 = asr::ctc_occupancy(plan(h, 8), 8);
         h->occ4 = asr::ctc_occupancy(plan(h, 4), 4);
-        h->occw = h->kcap <= 64 && asr::ctc_wave_supported(plan(h, -1), 0) ? asr::ctc_occupancy_wave(plan(h, -1)) : 0;
+        h->occw = h->kcap <= 128 && asr::ctc_wave_supported(plan(h, -1), 0) ? asr::ctc_occupancy_wave(plan(h, -1)) : 0;
     }
     if (h->ncu <= 0 || h->occ8 < 1 || h->occ4 < 1) return 8;
     const int u = (B + h->ncu - 1) / h->ncu;   // utterances on the busiest CU
@@ -522,7 +538,7 @@ int auto_waves(asr_ctc* h, int B) {
     const int n4 = h->occ4;
     const double cost4 = (u / n4) * rel_4w(n4) + (u % n4 ? rel_4w(u % n4) : 0.0);
     const int nw = h->occw;
-    const double costw = nw >= 1 ? (u / nw) * rel_w(nw) + (u % nw ? rel_w(u % nw) : 0.0) : 1e30;
+    const double costw = nw >= 1 ? (u / nw) * rel_w(nw, h->kcap) + (u % nw ? rel_w(u % nw, h->kcap) : 0.0) : 1e30;
     if (costw < cost4 && costw < cost8) return ASR_CTC_WAVES_LIST;
     return cost4 < cost8 ? 4 : 8;
 }
@@ -625,6 +641,11 @@ int status_code(const int* status, int B) {
 
 }  // namespace
 
+int asr_internal_ctc_wave_occupancy(asr_ctc* h) {
+    if (!h || h->cu_mode || h->ts || !asr::ctc_wave_supported(plan(h, -1), 0)) return 0;
+    return asr::ctc_occupancy_wave(plan(h, -1));
+}
+
 extern "C" {
 
 int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, int max_states,
@@ -687,6 +708,8 @@ int asr_ctc_destroy(asr_ctc_t* h) {
     hipFree(h->d_all_len);
     hipFree(h->d_all_ts);
     hipFree(h->d_stamps);
+    hipFree(h->d_seg);
+    for (auto e : h->seg_ev) hipEventDestroy(e);
     if (h->wide) asr_ctc_destroy(h->wide);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
@@ -758,16 +781,50 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
     return asr_ctc_decode_ex(h, d_emis, T, B, (long)B * h->V, h->V, nullptr, is_log, s);
 }
 
-int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long frame_stride,
-                      long utt_stride, const int32_t* h_lengths, int is_log, asr_stream_t s) {
-    if (!h || !d_emis || T < 1 || B < 1 || frame_stride < 1 || utt_stride < 1) return ASR_ERR_ARG;
-    if (h_lengths)
-        for (int b = 0; b < B; b++)
-            if (h_lengths[b] < 0 || h_lengths[b] > T) return ASR_ERR_ARG;
-    // timesteps are stored as 16-bit frame numbers next to the labels (slot
-    // tails, node records, ctc_trace.hip frame_field): frames >= 65536 would wrap
-    if (h->ts && T > ASR_CTC_TS_MAX_T) return ASR_ERR_UNSUPPORTED;
-    int rc = ensure_ws(h, B, T);
+}  // extern "C"
+
+namespace {
+
+int finish_decode(asr_ctc* h, hipStream_t st, int B, int T, int waves);
+
+// Queue the decode kernel (with its timing events) of frames [t0, t1).
+int launch_decode_events(asr_ctc* h, int waves, hipStream_t st, bool segmented) {
+    hipEvent_t e0 = h->ev0, e1 = h->ev1;
+    if (segmented) {   // one event pair per segment; last_kernel_ms sums them
+        const size_t need = 2 * (size_t)(h->nseg + 1);
+        while (h->seg_ev.size() < need) {
+            hipEvent_t e = nullptr;
+            ASR_HIP_TRY(hipEventCreate(&e));
+            h->seg_ev.push_back(e);
+        }
+        e0 = h->seg_ev[2 * h->nseg];
+        e1 = h->seg_ev[2 * h->nseg + 1];
+        h->nseg++;
+    }
+    ASR_HIP_TRY(hipEventRecord(e0, st));
+    int rc = asr::ctc_launch_decode(h->args, waves, st);
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(e1, st));
+    return ASR_OK;
+}
+
+// The decode of frames [t0, t1) of T: a whole decode (0, T, !segmented) or
+// one segment of asr_ctc_decode_segment.  Everything but the kernel launch
+// is set up at the first frame; the traceback follows the last.
+int decode_frames(asr_ctc* h, const float* d_emis, int T, int B, long frame_stride, long utt_stride,
+                  const int32_t* h_lengths, int is_log, asr_stream_t s, int t0, int t1, bool segmented) {
+    int rc = ASR_OK;
+    const hipStream_t st = asr_stream(s);
+    if (t0 > 0) {   // a later segment: the first one set everything up
+        h->args.emis = d_emis;
+        h->args.t0 = t0;
+        h->args.t1 = t1;
+        rc = launch_decode_events(h, ASR_CTC_WAVES_LIST, st, true);
+        if (rc) return rc;
+        if (t1 < T) return ASR_OK;
+        return finish_decode(h, st, B, T, ASR_CTC_WAVES_LIST);
+    }
+    rc = ensure_ws(h, B, T);
     if (rc) return rc;
     const hipStream_t st0 = asr_stream(s);
     if (h_lengths) {   // stage the lengths through pinned memory (stream-ordered)
@@ -789,6 +846,7 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     const long Beff = std::min<long>((long)B * h->concurrency, 1L << 30);
     int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h, (int)Beff));
     if (h->ts && waves < 0) waves = valid_waves(h, 8);
+    if (segmented) waves = ASR_CTC_WAVES_LIST;   // checked by the caller
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
@@ -810,6 +868,23 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     a.fin_ts = h->ts ? h->d_fin_ts : nullptr;
     a.tile0 = use_tile0(h) ? h->d_tile0 : nullptr;
     a.diag = h->diag;
+    a.t0 = 0;
+    a.t1 = segmented ? t1 : T;
+    a.seg_state = nullptr;
+    a.seg_bytes = 0;
+    if (segmented) {
+        const size_t sb = asr::ctc_seg_bytes_wave(a.g), need = sb * (size_t)B;
+        if (h->cap_seg < need) {
+            hipStreamSynchronize(st);
+            hipFree(h->d_seg);
+            h->d_seg = nullptr;
+            h->cap_seg = 0;
+            ASR_HIP_TRY(hipMalloc(&h->d_seg, need));
+            h->cap_seg = need;
+        }
+        a.seg_state = h->d_seg;
+        a.seg_bytes = (int)sb;
+    }
     // packed result layout for this (B, T)
     // The decode and traceback kernels write the packed results either
     // straight into the pinned host buffer (default: no copy to queue — a
@@ -837,27 +912,25 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
     }
     a.stamps = h->d_stamps;
 #endif
-    const hipStream_t st = asr_stream(s);
     // the previous traceback of this handle (on the result stream) reads the
     // node records this decode overwrites
     if (h->res_fork) ASR_HIP_TRY(hipStreamWaitEvent(st, h->ev_res, 0));
-    // ASR_PIPELINE_TRACE=1: host time of the enqueue steps over 0.5 ms (diagnostic)
-    static const bool trace = [] { const char* e = getenv("ASR_PIPELINE_TRACE"); return e && atoi(e); }();
-    auto tl = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!trace) return;
-        const auto now = std::chrono::steady_clock::now();
-        const double ms = std::chrono::duration<double, std::milli>(now - tl).count();
-        if (ms > 0.5) fprintf(stderr, "asr_ctc_decode: %s %.3f ms\n", what, ms);
-        tl = now;
-    };
-    ASR_HIP_TRY(hipEventRecord(h->ev0, st));
-    lap("event0");
-    rc = asr::ctc_launch_decode(a, waves, st);
+    h->nseg = 0;
+    h->have = false;
+    h->last_emis = d_emis;
+    h->last_tstride = frame_stride;
+    h->last_ustride = utt_stride;
+    h->last_lengths.assign(h_lengths ? h_lengths : nullptr, h_lengths ? h_lengths + B : nullptr);
+    h->last_is_log = is_log ? 1 : 0;
+    rc = launch_decode_events(h, waves, st, segmented);
     if (rc) return rc;
-    lap("launch");
-    ASR_HIP_TRY(hipEventRecord(h->ev1, st));
-    lap("event1");
+    if (segmented && t1 < T) return ASR_OK;
+    return finish_decode(h, st, B, T, waves);
+}
+
+// After the last frames: the best-path traceback and its results.
+int finish_decode(asr_ctc* h, hipStream_t st, int B, int T, int waves) {
+    asr::CtcArgs& a = h->args;
     // traceback and result copy: on the result stream when one is set, so
     // that the decode stream can start the next batch at once
     const hipStream_t rs = h->res_stream ? h->res_stream : st;
@@ -866,28 +939,71 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
         ASR_HIP_TRY(hipEventRecord(h->ev_dec, st));
         ASR_HIP_TRY(hipStreamWaitEvent(rs, h->ev_dec, 0));
     }
-    rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, rs);
+    int rc = asr::ctc_launch_best(a, h->d_codes, h->d_chain, rs);
     if (rc) return rc;
-    lap("traceback launch");
     // One copy of the packed results to the pinned mirror right behind the
     // traceback: asr_ctc_get_best waits for this event only, not for work the
     // caller queued on the stream afterwards (e.g. the next batch's decode).
     if (!h->res_direct)
         ASR_HIP_TRY(hipMemcpyAsync(h->h_res, h->d_res, 16 * (size_t)B + sizeof(int) * (size_t)B * T,
                                    hipMemcpyDeviceToHost, rs));
-    lap("result copy");
     ASR_HIP_TRY(hipEventRecord(h->ev_res, rs));
-    lap("event res");
     h->have = true;
-    h->last_emis = d_emis;
-    h->last_tstride = frame_stride;
-    h->last_ustride = utt_stride;
-    h->last_lengths.assign(h_lengths ? h_lengths : nullptr, h_lengths ? h_lengths + B : nullptr);
-    h->last_is_log = is_log ? 1 : 0;
     h->lastT = T;
     h->lastB = B;
     h->last_waves = waves;
     h->stream = st;
+    return ASR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long frame_stride,
+                      long utt_stride, const int32_t* h_lengths, int is_log, asr_stream_t s) {
+    if (!h || !d_emis || T < 1 || B < 1 || frame_stride < 1 || utt_stride < 1) return ASR_ERR_ARG;
+    if (h_lengths)
+        for (int b = 0; b < B; b++)
+            if (h_lengths[b] < 0 || h_lengths[b] > T) return ASR_ERR_ARG;
+    // timesteps are stored as 16-bit frame numbers next to the labels (slot
+    // tails, node records, ctc_trace.hip frame_field): frames >= 65536 would wrap
+    if (h->ts && T > ASR_CTC_TS_MAX_T) return ASR_ERR_UNSUPPORTED;
+    h->seg_next = 0;   // a whole decode ends any segmented one in progress
+    return decode_frames(h, d_emis, T, B, frame_stride, utt_stride, h_lengths, is_log, s, 0, T, false);
+}
+
+int asr_ctc_decode_segment(asr_ctc_t* h, const float* d_emis, int T, int t0, int t1, int B, long frame_stride,
+                           long utt_stride, const int32_t* h_lengths, int is_log, asr_stream_t s) {
+    if (!h || !d_emis || T < 1 || B < 1 || frame_stride < 1 || utt_stride < 1 || t0 < 0 || t1 <= t0 || t1 > T)
+        return ASR_ERR_ARG;
+    if (t0 != h->seg_next) return ASR_ERR_STATE;   // segments in order, starting at frame 0
+    if (t0 > 0 && (T != h->seg_T || B != h->seg_B || frame_stride != h->seg_fs || utt_stride != h->seg_us ||
+                   (is_log ? 1 : 0) != h->seg_is_log))
+        return ASR_ERR_ARG;
+    if (t0 == 0) {
+        if (h_lengths)
+            for (int b = 0; b < B; b++)
+                if (h_lengths[b] < 0 || h_lengths[b] > T) return ASR_ERR_ARG;
+        // the one-wave kernel carries the beam across segments: V <= 63, CPU
+        // semantics, no timesteps
+        if (h->ts || h->cu_mode || !asr::ctc_wave_supported(plan(h, ASR_CTC_WAVES_LIST), 0))
+            return ASR_ERR_UNSUPPORTED;
+    }
+    const int rc = decode_frames(h, d_emis, T, B, frame_stride, utt_stride, t0 == 0 ? h_lengths : nullptr,
+                                 is_log, s, t0, t1, true);
+    if (rc) {
+        h->seg_next = 0;
+        return rc;
+    }
+    if (t0 == 0) {
+        h->seg_T = T;
+        h->seg_B = B;
+        h->seg_fs = frame_stride;
+        h->seg_us = utt_stride;
+        h->seg_is_log = is_log ? 1 : 0;
+    }
+    h->seg_next = t1 < T ? t1 : 0;
     return ASR_OK;
 }
 
@@ -1033,6 +1149,17 @@ int asr_debug_ctc_stamps(asr_ctc_t* h, uint64_t* out) {
 int asr_ctc_last_kernel_ms(asr_ctc_t* h, float* ms) {
     if (!h || !ms) return ASR_ERR_ARG;
     if (!h->have) return ASR_ERR_STATE;
+    if (h->nseg > 0) {   // a segmented decode: the sum of its segments' kernels
+        float sum = 0.f;
+        for (int i = 0; i < h->nseg; i++) {
+            float x = 0.f;
+            ASR_HIP_TRY(hipEventSynchronize(h->seg_ev[2 * i + 1]));
+            ASR_HIP_TRY(hipEventElapsedTime(&x, h->seg_ev[2 * i], h->seg_ev[2 * i + 1]));
+            sum += x;
+        }
+        *ms = sum;
+        return ASR_OK;
+    }
     ASR_HIP_TRY(hipEventSynchronize(h->ev1));
     ASR_HIP_TRY(hipEventElapsedTime(ms, h->ev0, h->ev1));
     return ASR_OK;

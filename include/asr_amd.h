@@ -212,6 +212,30 @@ int asr_ctc_decode(asr_ctc_t* h, const float* d_emis, int T, int B, int is_log, 
 int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long frame_stride,
                       long utt_stride, const int32_t* h_lengths, int is_log, asr_stream_t s);
 
+/* Segmented (streaming) decode — no reference counterpart (the reference
+ * decodes whole utterances, CTCBeamSearch.cu:262-312): frames [t0, t1) of a
+ * T-frame batch, the beam of every utterance carried on the device from one
+ * segment to the next, so a producer can hand over emissions segment by
+ * segment and the decode of a batch starts after its first T/S frames.
+ * Segments come in order on one handle: t0 = 0 first (h_lengths is read
+ * then), each next t0 = the previous t1, the last ends at t1 = T; then the
+ * results are fetched as after asr_ctc_decode (asr_ctc_get_best ...; before
+ * that, ASR_ERR_STATE).  d_emis addresses frame t0: element (t, b, v) of the
+ * segment is d_emis[(t - t0)*frame_stride + b*utt_stride + v].  T, B, the
+ * strides and is_log must be the same for every segment.  Results are
+ * bit-identical to a whole decode of the same frames.  Runs the one-wave
+ * kernel (ASR_CTC_WAVES_LIST): V <= 63, CPU semantics, timesteps off, else
+ * ASR_ERR_UNSUPPORTED; ASR_ERR_STATE for a segment out of order.  Overflow
+ * retry (automatic capacity): asr_ctc_get_best re-decodes the whole batch
+ * from the FIRST segment's d_emis over T frames, so that pointer must then
+ * address all T frames (e.g. segments of one [T][B][V] buffer); a caller
+ * with a ring buffer creates the handle with an explicit max_states (an
+ * overflow is then reported as ASR_ERR_BEAM_OVERFLOW).
+ * asr_ctc_last_kernel_ms reports the sum of the segments' kernel times. */
+int asr_ctc_decode_segment(asr_ctc_t* h, const float* d_emis, int T, int t0, int t1, int B,
+                           long frame_stride, long utt_stride, const int32_t* h_lengths, int is_log,
+                           asr_stream_t s);
+
 /* Best hypothesis of each utterance (cpp:74-84: max score, first in string
  * order on ties).  Synchronises the decode stream.  h_labels[B][max_len]
  * (label ids), h_lengths[B], h_logp[B] (fp64 log-probability).
@@ -299,6 +323,11 @@ typedef struct asr_pipeline_config {
     int prod_streams;    /* production streams (0 = automatic) */
     int decode_cus;      /* chip-filling batches: CUs given to decoding (0 = automatic,
                             -1 = every stream on every CU) */
+    int segments;        /* T-segments per batch (0 = automatic, 1 = whole utterances): the
+                            fused production hands emissions over segment by segment and
+                            the decode of a batch starts after its first T / segments
+                            frames (asr_ctc_decode_segment); chip-filling batches with the
+                            fused production only, else 1 */
 } asr_pipeline_config;
 int asr_pipeline_create(const asr_pipeline_config* cfg, const float* d_W_ih, const float* d_W_hh,
                         const float* d_b_ih, const float* d_b_hh, const float* d_W_out,
@@ -325,7 +354,9 @@ int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
 /* The schedule chosen: mode (0 CU groups for small batches, 1 chip-filling
  * batches, 2 CU groups for H > 256), decodes in flight, production streams,
  * CUs per decode group / decode partition, and the decoder's waves per
- * utterance in the last decode.  Any pointer may be NULL. */
+ * utterance in the last decode.  Any pointer may be NULL.
+ * asr_pipeline_get_segments: T-segments per batch in use. */
+int asr_pipeline_get_segments(asr_pipeline_t* p, int* segments);
 int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod_streams, int* decode_cus,
                           int* decode_waves);
 /* How the pipeline produces a batch's emissions: fused = 1 when the

@@ -181,3 +181,31 @@ def test_pipeline_failure_is_reported(B, stage, monkeypatch):
         with pytest.raises(asr.AsrError):
             p.submit(xs[4])
     p.close()
+
+
+@pytest.mark.parametrize("segments,B", [(2, 300), (3, 600), (5, 256)])
+def test_pipeline_segmented_handoff(segments, B):
+    """T-segmented handoff (asr_pipeline_config.segments): the fused
+    production publishes each segment's emissions and the decode of that
+    segment starts behind it (asr_ctc_decode_segment), the recurrence
+    carrying h across segments.  Same bits as the sequential fused
+    production + whole decode, batch for batch."""
+    T, inp, H, V, beam = 37, 48, 64, 29, 40
+    W = _weights(inp, H, V, seed=segments)
+    rng = np.random.default_rng(segments)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(4)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W, segments=segments)
+    d = p.describe()
+    assert d["mode"] == "chip-filling batches" and d["fused_emission"] and d["segments"] == segments, d
+    for x in xs:
+        p.submit(x)
+    got = []
+    while p.pending():
+        lab, ln, lp, ms = p.collect()
+        assert ms > 0.0
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    assert p.describe()["decode_waves"] == asr.ASR_CTC_WAVES_LIST
+    p.close()
+    for g, x in zip(got, xs):
+        ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])

@@ -36,6 +36,12 @@ if [ -n "${RUNS:-}" ]; then
     rc=${PIPESTATUS[0]}
     [ $rc -eq 0 ] || exit $rc
 fi
+if [ -n "${EXTRA:-}" ]; then   # one more GPU command (e.g. a tools/ sweep), its own limit
+    echo "== extra: $EXTRA" | tee -a "$O/session.log"
+    timeout -k 10 ${EXTRA_LIMIT:-300} bash -c "$EXTRA" > "$O/extra.log" 2>&1
+    rc=$?; echo "extra rc=$rc" | tee -a "$O/session.log"; tail -30 "$O/extra.log"
+    stop_if_fatal $rc extra
+fi
 if [ -n "${PASSES:-}" ]; then
     echo "== rocprofv3 ${PASSES}" | tee -a "$O/session.log"
     BENCH_ARGS="${PROF_ARGS:---steps 5 --warmup 2 --no-cpu-baseline}" OUT="$OUT" bash tools/profile_bench.sh \
