@@ -198,7 +198,10 @@ def load_profile_json(name: str):
         return None
 
 
-PROFILE_ROUND = "r03"   # profiles/<round>/ holds the counter summaries this line embeds
+# profiles/<round>/ hold the counter summaries this line embeds: the newest
+# round that profiled the workload and kernel variant (every record names its
+# source run and commit)
+PROFILE_ROUNDS = ("r04", "r03")
 
 
 def decoder_variant(V: int, waves: int, max_states: int) -> str:
@@ -220,12 +223,27 @@ def load_counters(name: str, workload: str, variant: str):
     passes over this bench) for exactly this workload and kernel variant, with
     the run it came from; None when that pair was not profiled (a changed
     kernel or schedule never picks up stale counters)."""
-    d = load_profile_json(f"{PROFILE_ROUND}/{name}.json")
-    try:
-        rec = d[workload][variant]
-    except Exception:
-        return None
-    return dict(rec, workload=workload, variant=variant)
+    for rnd in PROFILE_ROUNDS:
+        d = load_profile_json(f"{rnd}/{name}.json")
+        try:
+            rec = d[workload][variant]
+        except Exception:
+            continue
+        if name == "issue" and "issue" not in rec and "valu_mix" not in rec:
+            continue
+        return dict(rec, workload=workload, variant=variant, round=rnd)
+    return None
+
+
+def load_mfma_counters(workload: str):
+    """Counter evidence of the dense kernels (profiles/<round>/mfma.json, from
+    tools/mfma_from_pmc.py over a rocprofv3 --pmc pass of this bench):
+    per kernel, MFMA busy cycles against the CUs' matrix-pipe cycles."""
+    for rnd in PROFILE_ROUNDS:
+        d = load_profile_json(f"{rnd}/mfma.json")
+        if d and workload in d:
+            return dict(d[workload], round=rnd)
+    return None
 
 
 def cpu_share():
@@ -810,6 +828,21 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
     if rank == 0 and world == 1 and not args.decode_only:
         mfma = measure_gemms(asr, d_x, d_wih, d_hid0, d_wout, d_bout, d_emis0, T, B, In, H, V,
                              fused=(d_whh, d_bih, d_bhh) if (sched or {}).get("fused_emission") else None)
+        pmc = load_mfma_counters(args.config)
+        if pmc:   # the rocprofv3 counters of the same stages (MFMA busy cycles, clock)
+            ks = pmc.get("kernels", {})
+
+            def pick(prefix, biggest=True):
+                lst = [r for k, v in ks.items() if k.startswith(prefix) for r in v]
+                return max(lst, key=lambda r: r["gflop"]) if lst else None
+            for stage, kern in (("input_gemm", "gemm_wide_kernel"), ("emission_gemm", "gemm_narrow_kernel"),
+                                ("recurrence_emission", "rnn_recur_mfma_kernel<true>")):
+                r = pick(kern)
+                if stage in mfma and r:
+                    mfma[stage]["counters"] = {k: r[k] for k in ("mfma_busy", "cus", "gflop", "clock_ghz",
+                                                                 "duration_ms", "dispatches")}
+            mfma["counters_source"] = {"source": pmc.get("source"), "round": pmc.get("round"),
+                                       "note": pmc.get("note")}
 
     cpu = None
     parity = None

@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--B", type=int, required=True)
     ap.add_argument("--workload", default="C2")
     ap.add_argument("--source", default="")
-    ap.add_argument("--round", default="r03")
+    ap.add_argument("--round", default="r04")
     ap.add_argument("--cus", type=int, default=0, help="CUs the decode ran on (default: B)")
     args = ap.parse_args()
     per = {}   # dispatch -> counter -> value
@@ -86,7 +86,7 @@ def main():
     p = Path(__file__).resolve().parents[1] / "profiles" / args.round / "issue.json"
     p.parent.mkdir(parents=True, exist_ok=True)
     allw = json.loads(p.read_text()) if p.exists() else {}
-    allw.setdefault(args.workload, {})[variant] = out
+    allw.setdefault(args.workload, {}).setdefault(variant, {}).update(out)   # keeps a valu_mix entry
     p.write_text(json.dumps(allw, indent=1))
     print(json.dumps(out, indent=1))
 
