@@ -58,7 +58,7 @@ EXPORTS = [
     "asr_ctc_set_concurrency", "asr_rnn_set_recurrence", "asr_rnn_get_recurrence",
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
     "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams",
-    "asr_pipeline_peek_emissions", "asr_pipeline_get_segments",
+    "asr_pipeline_peek_emissions", "asr_pipeline_get_segments", "asr_pipeline_get_groups",
     "asr_pipeline_destroy",
 ]
 
@@ -127,6 +127,7 @@ def lib() -> ctypes.CDLL:
         "asr_pipeline_get_streams": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_pipeline_peek_emissions": [_vp, ctypes.POINTER(_vp)],
         "asr_pipeline_get_segments": [_vp, ctypes.POINTER(_i)],
+        "asr_pipeline_get_groups": [_vp, ctypes.POINTER(_i)],
         "asr_rnn_bidir_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_ctc_create": [_vp, _i, _i, _i, _i, ctypes.POINTER(_vp)],
         "asr_ctc_destroy": [_vp],
@@ -598,13 +599,14 @@ class Pipeline:
         fz, gr, rk = _i(), ctypes.c_longlong(), _i()
         check(lib().asr_pipeline_get_production(self.h, ctypes.byref(fz), ctypes.byref(gr), ctypes.byref(rk)),
               "asr_pipeline_get_production")
-        ns, hq, sg = _i(), _i(), _i()
+        ns, hq, sg, gr = _i(), _i(), _i(), _i()
         check(lib().asr_pipeline_get_streams(self.h, ctypes.byref(ns), ctypes.byref(hq)), "asr_pipeline_get_streams")
         check(lib().asr_pipeline_get_segments(self.h, ctypes.byref(sg)), "asr_pipeline_get_segments")
+        check(lib().asr_pipeline_get_groups(self.h, ctypes.byref(gr)), "asr_pipeline_get_groups")
         return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
                 "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
                 "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
-                "hw_queues": hq.value, "segments": sg.value}
+                "hw_queues": hq.value, "segments": sg.value, "groups": gr.value}
 
     def submit(self, x: "DeviceMatrix") -> None:
         """Queue a batch.  x is kept alive here until its batch is collected

@@ -41,6 +41,14 @@ extern thread_local int asr_internal_gemm_tiled;
 // apply (V > 63, .cu semantics, timesteps).  For the pipeline's schedule.
 struct asr_ctc;
 int asr_internal_ctc_wave_occupancy(asr_ctc* h);
+// The recurrence (h0 = 0) of nb <= 4 equal-shape batches at once, in place
+// over each hids[j] [T*B, H] (holding x.W_ih on entry): H > 256 runs one
+// per-frame MFMA step launch for all of them (the step is latency-bound, so
+// a step of 2-4 batches costs about one); bit-identical to nb separate
+// asr_rnn_recur_fwd calls.  ASR_ERR_UNSUPPORTED for H <= 256 with nb > 1 or
+// B % 16 != 0.
+int asr_internal_rnn_recur_multi(const float* W_hh, const float* b_ih, const float* b_hh, float* const* hids,
+                                 int nb, int T, int B, int H, hipStream_t st);
 
 // Order-preserving bijection fp64 <-> u64: a < b  <=>  key(a) < key(b).
 // -0.0 is folded onto +0.0 (they compare equal as doubles).  Key 0 is never

@@ -44,6 +44,11 @@ int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);
 // MFMA recurrence step (H % 128 == 0); ASR_ERR_UNSUPPORTED otherwise.
 int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                          const float* b_hh, int B, int H, hipStream_t s);
+constexpr int STEP_MAXB = 4;
+// The same step for nb <= STEP_MAXB batches of B rows at once (one launch; batch j:
+// h_t at hts[j], h_{t-1} at hps[j]); nb > 1 needs B % 16 == 0.  Same bits.
+int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int nb, const float* Whh,
+                               const float* b_ih, const float* b_hh, int B, int H, hipStream_t s);
 int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                     const float* b_hh, int B, int H, hipStream_t s);
 

@@ -995,10 +995,19 @@ int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b
 // tiles re-read h_{t-1} and W_hh fewer times (BL, B = 256, H = 2048:
 // 16-column tiles read 384 MB per step from L2 for a 2 GFLOP product).
 // Grid (H / (16 NT), ceil(B / (16 RB))).
+// Several batches in one step (StepRows, the pipeline's production groups,
+// DESIGN.md §7d): batch j's rows are row tiles [j * tiles, (j + 1) * tiles)
+// of the grid, with its own h_t / h_{t-1} pointers; B % (16 RB) == 0 then, so
+// no tile straddles two batches.  Every row's arithmetic is the one-batch
+// kernel's, so grouping never changes a bit.
 constexpr int RSM_WAVES = 8;
+struct StepRows {
+    float* ht[STEP_MAXB];
+    const float* hp[STEP_MAXB];
+    int tiles;   // row tiles per batch
+};
 template <int RB, int NT>
-__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __restrict__ ht,
-                                                                      const float* __restrict__ hp,
+__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(StepRows sr,
                                                                       const float* __restrict__ Whh,
                                                                       const float* __restrict__ b_ih,
                                                                       const float* __restrict__ b_hh,
@@ -1006,7 +1015,10 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __
     __shared__ f32x4 part[RSM_WAVES][RB * NT][64];
     constexpr int CH = (RB * NT >= 4) ? 4 : 8;   // 16-k chunks whose loads are in flight together
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n0 = blockIdx.x * (16 * NT), r0 = blockIdx.y * (16 * RB);
+    const int bj = (int)blockIdx.y / sr.tiles;
+    float* __restrict__ ht = sr.ht[bj];
+    const float* __restrict__ hp = sr.hp[bj];
+    const int n0 = blockIdx.x * (16 * NT), r0 = ((int)blockIdx.y - bj * sr.tiles) * (16 * RB);
     const int g = lane >> 4, c = lane & 15;
     const int kw = H / RSM_WAVES, kbeg = w * kw, nchunk = kw / 16;
     const float* arow[RB];
@@ -1073,35 +1085,51 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_step_mfma_kernel(float* __
 }
 
 template <int RB, int NT>
-static void launch_step_mfma(float* ht, const float* hp, const float* Whh, const float* b_ih, const float* b_hh,
+static void launch_step_mfma(StepRows sr, int nb, const float* Whh, const float* b_ih, const float* b_hh,
                              int B, int H, hipStream_t s) {
-    hipLaunchKernelGGL((rnn_step_mfma_kernel<RB, NT>), dim3((unsigned)(H / (16 * NT)), (unsigned)((B + 16 * RB - 1) / (16 * RB))),
-                       dim3(64 * RSM_WAVES), 0, s, ht, hp, Whh, b_ih, b_hh, B, H);
+    sr.tiles = (B + 16 * RB - 1) / (16 * RB);
+    hipLaunchKernelGGL((rnn_step_mfma_kernel<RB, NT>), dim3((unsigned)(H / (16 * NT)), (unsigned)(nb * sr.tiles)),
+                       dim3(64 * RSM_WAVES), 0, s, sr, Whh, b_ih, b_hh, B, H);
 }
 
 int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                          const float* b_hh, int B, int H, hipStream_t s) {
-    if (B <= 0 || H <= 0 || (H % 128) != 0) return ASR_ERR_UNSUPPORTED;
-    if ((uintptr_t)hp % 16 != 0) return ASR_ERR_UNSUPPORTED;   // float4 rows
+    return rnn_step_mfma_multi_launch(&ht, &hp, 1, Whh, b_ih, b_hh, B, H, s);
+}
+
+int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int nb, const float* Whh,
+                               const float* b_ih, const float* b_hh, int B, int H, hipStream_t s) {
+    if (B <= 0 || H <= 0 || (H % 128) != 0 || nb < 1 || nb > STEP_MAXB) return ASR_ERR_UNSUPPORTED;
+    StepRows sr{};
+    for (int j = 0; j < nb; j++) {
+        if ((uintptr_t)hps[j] % 16 != 0) return ASR_ERR_UNSUPPORTED;   // float4 rows
+        sr.ht[j] = hts[j];
+        sr.hp[j] = hps[j];
+    }
+    // several batches: whole row tiles per batch
+    if (nb > 1 && B % 16 != 0) return ASR_ERR_UNSUPPORTED;
+    const int Btot = B * nb;
     // ASR_RNN_STEP_NT=1/2/4 forces the column tiles per workgroup (A/B)
     const char* fe = getenv("ASR_RNN_STEP_NT");
     int nt = fe ? atoi(fe) : 0;
-    const long nb16 = (B + 15) / 16, nb32 = (B + 31) / 32;
+    const long nb16 = (Btot + 15) / 16, nb32 = (Btot + 31) / 32;
+    const bool rb2 = nb == 1 || B % 32 == 0;   // 32-row tiles must not straddle batches
     if (nt != 1 && nt != 2 && nt != 4) {
         // the widest tiles that still give every CU a workgroup (256 CUs:
         // BL's 256 x 2048 -> 32 x 8 = 256 workgroups of 32 x 64); narrow
         // tiles for small B (C5's 32 x 1024: latency-bound, 64 x 2)
         nt = (H / 64) * nb32 >= 256 ? 4 : ((H / 32) * nb32 >= 256 ? 2 : 1);
     }
+    if (!rb2) nt = 1;
     if (nt == 4) {
-        launch_step_mfma<2, 4>(ht, hp, Whh, b_ih, b_hh, B, H, s);
+        launch_step_mfma<2, 4>(sr, nb, Whh, b_ih, b_hh, B, H, s);
     } else if (nt == 2) {
-        launch_step_mfma<2, 2>(ht, hp, Whh, b_ih, b_hh, B, H, s);
-    } else if ((H / 16) * nb16 <= 512) {   // 16-row tiles while that is <= 2 per CU
-        launch_step_mfma<1, 1>(ht, hp, Whh, b_ih, b_hh, B, H, s);
+        launch_step_mfma<2, 2>(sr, nb, Whh, b_ih, b_hh, B, H, s);
+    } else if ((H / 16) * nb16 <= 512 || !rb2) {   // 16-row tiles while that is <= 2 per CU
+        launch_step_mfma<1, 1>(sr, nb, Whh, b_ih, b_hh, B, H, s);
     } else {   // 32-row tiles (measured: 16-row tiles win up to ~2 workgroups per CU, 64-row
                // tiles and 16 waves per workgroup lose everywhere)
-        launch_step_mfma<2, 1>(ht, hp, Whh, b_ih, b_hh, B, H, s);
+        launch_step_mfma<2, 1>(sr, nb, Whh, b_ih, b_hh, B, H, s);
     }
     ASR_LAUNCH_TRY();
     return ASR_OK;

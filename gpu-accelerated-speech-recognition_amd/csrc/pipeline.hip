@@ -25,8 +25,9 @@
 //           with the emission projection fused (asr_rnn_emit_fwd, V <= 32),
 //           part of the input projection optionally on the decode CUs.
 //   GROUPS2 H > 256 (C5: 2000 per-frame recurrence launches, replayed from
-//           the library's HIP graph): D = 2 decode groups, 2 production
-//           streams on the remaining CUs.
+//           the library's HIP graph): the recurrences of G = 2 consecutive
+//           batches run as one (production groups), D = 2G decode groups,
+//           2 production streams on the remaining CUs.
 // Results come back in submission order (asr_pipeline_collect).  A batch's
 // buffers are reused only after its results were fetched (the decoder's
 // overflow retry re-reads its emissions): submit collects internally when
@@ -69,6 +70,8 @@ struct asr_pipeline {
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
     bool gtiled = false;  // ... with the tiled GEMM kernel (several decodes in flight)
     int S = 1;            // T-segments per batch (fused production only)
+    int G = 1;            // GROUPS2: batches whose recurrences run as one (a production group)
+    std::vector<long> group;          // batches whose input projection is queued, recurrence not yet
     std::vector<float*> hst;          // [nbuf][B][H] the recurrence's h at a segment end
     std::vector<hipEvent_t> ev_seg;   // [nbuf][S] segment s of buffer k's emissions ready
     hipStream_t s_gdec = nullptr;   // the decode CUs' share of the input projections
@@ -283,6 +286,42 @@ int enqueue_decode(asr_pipeline* p, long i) {
     return ASR_OK;
 }
 
+// Production groups (GROUPS2, H > 256: C5): the recurrence is T dependent
+// step launches whose time hardly depends on B (latency-bound), so the
+// recurrences of G consecutive batches run as one (asr_internal_rnn_recur_multi:
+// one step launch for all of them per frame).  Part 1 at each submit: the
+// batch's input projection, on its group's production stream.
+int produce_group_head(asr_pipeline* p, long i, const float* x) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
+    hipStream_t sp = p->s_prod[(i / p->G) % p->P];
+    ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    return asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], c.T * c.B, c.in, c.H, ASR_EPI_NONE, sp);
+}
+
+// Part 2, once the group is complete (or a fetch needs a member): one
+// recurrence over the group, each member's emission projection, its decode.
+int flush_group(asr_pipeline* p) {
+    if (p->group.empty()) return ASR_OK;
+    const auto& c = p->cfg;
+    std::vector<long> g;
+    g.swap(p->group);
+    hipStream_t sp = p->s_prod[(g[0] / p->G) % p->P];
+    float* hids[4];
+    for (size_t j = 0; j < g.size(); j++) hids[j] = p->hid[g[j] % p->nbuf];
+    int rc = asr_internal_rnn_recur_multi(p->W_hh, p->b_ih, p->b_hh, hids, (int)g.size(), c.T, c.B, c.H, sp);
+    for (size_t j = 0; j < g.size() && !rc; j++) {
+        const int k = (int)(g[j] % p->nbuf);
+        rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
+                            ASR_EPI_BIAS_LOGSOFTMAX, sp);
+        if (!rc && hipEventRecord(p->ev_ready[k], sp) != hipSuccess) rc = ASR_ERR_HIP;
+        if (!rc) rc = enqueue_decode(p, g[j]);
+    }
+    if (rc) set_failed(p, g[0], rc);   // the group's batches were accepted: no results can come
+    return rc;
+}
+
 // Queue the emission GEMM and decode of the batch whose production was split.
 int flush_tail(asr_pipeline* p) {
     if (p->pending_tail < 0) return ASR_OK;
@@ -311,6 +350,7 @@ int fetch(asr_pipeline* p, Result& r) {
     if (p->fail_from >= 0 && j >= p->fail_from) return p->fail_rc;
     if (j >= p->decoded) {
         int rc = flush_tail(p);
+        if (!rc) rc = flush_group(p);
         if (rc) return rc;
     }
     if (j >= p->decoded) return ASR_ERR_INTERNAL;   // never queued (cannot happen once flushed)
@@ -443,7 +483,14 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
         p->gcu = bcu;
-        p->D = c.inflight ? c.inflight : std::max(1, std::min(2, ncu / bcu - 1));
+        // production groups: G batches' recurrences as one (H > 256, the
+        // per-frame step launches; rows in whole 16-row tiles), default 2
+        // (ASR_PIPELINE_GROUP: A/B).  A step of 2 batches costs about one,
+        // so production keeps up with ~2x the decodes: D = 2G.
+        const char* ge = getenv("ASR_PIPELINE_GROUP");
+        const int Gw = ge ? atoi(ge) : 2;
+        p->G = (c.H > 256 && (c.H % 128) == 0 && (c.B % 16) == 0) ? std::max(1, std::min(4, Gw)) : 1;
+        p->D = c.inflight ? c.inflight : std::max(1, std::min(2 * p->G, ncu / bcu - 1));
         p->P = c.prod_streams ? c.prod_streams : (c.H > 256 ? 2 : 1);
         if (p->D == 1) p->gcu = 0;
     } else {   // chip-filling batches otherwise (C3's beam 100, BL's H = 2048): one decode at a time
@@ -488,6 +535,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // D decoding + P producing (+1: split production queues the next input
     // projection before the previous batch's emission projection)
     p->nbuf = p->D + p->P + (p->split ? 1 : 0);
+    if (p->G > 1) p->nbuf = p->D + (p->P + 1) * p->G;   // P groups producing, one filling, D decoding
     if (p->nbuf < 2) p->nbuf = 2;
     // streams
     auto mk = [&](hipStream_t* s, int lo, int hi) { return rc ? rc : (rc = cu_stream(s, ncu, lo, hi)); };
@@ -581,6 +629,14 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
         rc = flush_tail(p);   // the previous batch: emission GEMM after this batch's input GEMM
         if (trace) lap("tail+decode", last);
         p->pending_tail = i;
+    } else if (p->G > 1) {
+        rc = produce_group_head(p, i, x);
+        if (trace) lap("group head", last);
+        if (rc) return rc;
+        p->submitted = i + 1;
+        p->group.push_back(i);
+        if ((int)p->group.size() == p->G) rc = flush_group(p);
+        if (trace) lap("group", last);
     } else {
         rc = p->fuse ? produce_fused(p, i, x) : produce_full(p, i, x);
         if (trace) lap("produce", last);
@@ -656,6 +712,12 @@ int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode
     if (fused) *fused = p->fuse ? 1 : 0;
     if (decode_cu_rows) *decode_cu_rows = p->fuse ? p->grows : 0;
     if (recurrence) *recurrence = p->rnn_kind >= 0 ? p->rnn_kind : ASR_RNN_RECUR_AUTO;
+    return ASR_OK;
+}
+
+int asr_pipeline_get_groups(asr_pipeline_t* p, int* group) {
+    if (!p || !group) return ASR_ERR_ARG;
+    *group = p->G;
     return ASR_OK;
 }
 

@@ -204,7 +204,7 @@ static bool rnn_use_mfma(int B, int H) {
 // Recurrence over a hid buffer that already holds the input projection
 // P_t = x_t . W_ih, in place: hid[t] = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)).
 static int rnn_frames_eager(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
-                            float* hid, int T, int B, int H, hipStream_t st);
+                            float* const* hids, int nb, int T, int B, int H, hipStream_t st);
 
 // The T per-frame launches of a (pointers, shape) recurrence, captured once
 // into a HIP graph and replayed: the host then queues one graph launch per
@@ -215,11 +215,16 @@ static int rnn_frames_eager(const float* h0, const float* W_hh, const float* b_i
 // captured into that graph as they are).  A small cache, evicting the least
 // recently used.  ASR_RNN_GRAPH=0: always eager (A/B).
 struct RecurGraphKey {
-    int dev, T, B, H;
-    const void *h0, *W_hh, *b_ih, *b_hh, *hid;
+    int dev, T, B, H, nb;
+    const void *h0, *W_hh, *b_ih, *b_hh;
+    const void* hid[asr::STEP_MAXB];
     bool operator==(const RecurGraphKey& o) const {
-        return dev == o.dev && T == o.T && B == o.B && H == o.H && h0 == o.h0 && W_hh == o.W_hh &&
-               b_ih == o.b_ih && b_hh == o.b_hh && hid == o.hid;
+        if (!(dev == o.dev && T == o.T && B == o.B && H == o.H && nb == o.nb && h0 == o.h0 && W_hh == o.W_hh &&
+              b_ih == o.b_ih && b_hh == o.b_hh))
+            return false;
+        for (int j = 0; j < nb; j++)
+            if (hid[j] != o.hid[j]) return false;
+        return true;
     }
 };
 struct RecurGraph {
@@ -234,13 +239,17 @@ static unsigned long g_graph_tick = 0;
 constexpr size_t RECUR_GRAPH_CACHE = 8;
 
 static int rnn_recurrence_frames(const float* h0, const float* W_hh, const float* b_ih,
-                                 const float* b_hh, float* hid, int T, int B, int H, hipStream_t st) {
+                                 const float* b_hh, float* const* hids, int nb, int T, int B, int H,
+                                 hipStream_t st) {
     const char* ge = getenv("ASR_RNN_GRAPH");
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if ((ge && ge[0] == '0') || T < 8 || hipStreamIsCapturing(st, &cap) != hipSuccess ||
         cap != hipStreamCaptureStatusNone)
-        return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
-    RecurGraphKey key{0, T, B, H, h0, W_hh, b_ih, b_hh, hid};
+        return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hids, nb, T, B, H, st);
+    RecurGraphKey key{};
+    key.T = T; key.B = B; key.H = H; key.nb = nb;
+    key.h0 = h0; key.W_hh = W_hh; key.b_ih = b_ih; key.b_hh = b_hh;
+    for (int j = 0; j < nb; j++) key.hid[j] = hids[j];
     ASR_HIP_TRY(hipGetDevice(&key.dev));
     std::lock_guard<std::mutex> lock(g_graph_mu);
     RecurGraph* e = nullptr;
@@ -258,7 +267,7 @@ static int rnn_recurrence_frames(const float* h0, const float* W_hh, const float
     }
     e->last = ++g_graph_tick;
     if (++e->uses < 2 && !e->exec)   // first use: eager (kernel attributes set, nothing captured for one-offs)
-        return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+        return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hids, nb, T, B, H, st);
     if (!e->exec) {
         hipStream_t cs;
         ASR_HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
@@ -266,7 +275,7 @@ static int rnn_recurrence_frames(const float* h0, const float* W_hh, const float
         int rc = ASR_OK;
         hipError_t he = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
         if (he == hipSuccess) {
-            rc = rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, cs);
+            rc = rnn_frames_eager(h0, W_hh, b_ih, b_hh, hids, nb, T, B, H, cs);
             he = hipStreamEndCapture(cs, &graph);
         }
         if (he == hipSuccess && rc == ASR_OK) he = hipGraphInstantiate(&e->exec, graph, nullptr, nullptr, 0);
@@ -275,7 +284,7 @@ static int rnn_recurrence_frames(const float* h0, const float* W_hh, const float
         if (rc) return rc;
         if (he != hipSuccess) {   // no graph: stay eager for this key
             e->exec = nullptr;
-            return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+            return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hids, nb, T, B, H, st);
         }
     }
     ASR_HIP_TRY(hipGraphLaunch(e->exec, st));
@@ -288,15 +297,33 @@ static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
         if (rnn_use_mfma(B, H)) return asr::rnn_recur_mfma_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
         return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
     }
-    return rnn_recurrence_frames(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
+    return rnn_recurrence_frames(h0, W_hh, b_ih, b_hh, &hid, 1, T, B, H, st);
 }
 
 // H > 256: one small-M step kernel per frame, h_t = tanh((P_t +
 // h_{t-1}.W_hh) + bias) in place: MFMA with an 8-way K split when
 // H % 128 == 0, else the VALU kernel with W_hh slices in LDS.
 static int rnn_frames_eager(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
-                            float* hid, int T, int B, int H, hipStream_t st) {
+                            float* const* hids, int nb, int T, int B, int H, hipStream_t st) {
     int rc = ASR_OK;
+    if (nb > 1) {   // several batches per step (h0 = zeros): one MFMA step launch for all
+        if (h0 || (H & 127) != 0 || (B & 15) != 0 || nb > asr::STEP_MAXB) return ASR_ERR_UNSUPPORTED;
+        for (int t = 0; t < T && !rc; t++) {
+            float* hts[asr::STEP_MAXB];
+            const float* hps[asr::STEP_MAXB];
+            for (int j = 0; j < nb; j++) {
+                hts[j] = hids[j] + (size_t)t * B * H;
+                hps[j] = t ? hids[j] + (size_t)(t - 1) * B * H : nullptr;
+            }
+            if (t == 0) {
+                for (int j = 0; j < nb && !rc; j++) rc = asr::bias_tanh_launch(hts[j], b_ih, b_hh, (long)B * H, H, st);
+            } else {
+                rc = asr::rnn_step_mfma_multi_launch(hts, hps, nb, W_hh, b_ih, b_hh, B, H, st);
+            }
+        }
+        return rc;
+    }
+    float* hid = hids[0];
     for (int t = 0; t < T; t++) {
         float* ht = hid + (size_t)t * B * H;
         const float* hp = t == 0 ? h0 : hid + (size_t)(t - 1) * B * H;
@@ -640,6 +667,13 @@ int status_code(const int* status, int B) {
 }
 
 }  // namespace
+
+int asr_internal_rnn_recur_multi(const float* W_hh, const float* b_ih, const float* b_hh, float* const* hids,
+                                 int nb, int T, int B, int H, hipStream_t st) {
+    if (nb == 1) return rnn_recurrence(nullptr, W_hh, b_ih, b_hh, hids[0], T, B, H, st);
+    if (H <= 256) return ASR_ERR_UNSUPPORTED;   // the register-resident kernels: one batch each
+    return rnn_recurrence_frames(nullptr, W_hh, b_ih, b_hh, hids, nb, T, B, H, st);
+}
 
 int asr_internal_ctc_wave_occupancy(asr_ctc* h) {
     if (!h || h->cu_mode || h->ts || !asr::ctc_wave_supported(plan(h, -1), 0)) return 0;

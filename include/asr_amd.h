@@ -355,8 +355,12 @@ int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
  * batches, 2 CU groups for H > 256), decodes in flight, production streams,
  * CUs per decode group / decode partition, and the decoder's waves per
  * utterance in the last decode.  Any pointer may be NULL.
- * asr_pipeline_get_segments: T-segments per batch in use. */
+ * asr_pipeline_get_segments: T-segments per batch in use.
+ * asr_pipeline_get_groups: batches whose recurrences run as one (mode 2,
+ * H > 256: one per-frame step launch for G batches; a batch's production
+ * then starts when its group is complete or its results are asked for). */
 int asr_pipeline_get_segments(asr_pipeline_t* p, int* segments);
+int asr_pipeline_get_groups(asr_pipeline_t* p, int* group);
 int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod_streams, int* decode_cus,
                           int* decode_waves);
 /* How the pipeline produces a batch's emissions: fused = 1 when the

@@ -209,3 +209,33 @@ def test_pipeline_segmented_handoff(segments, B):
     for g, x in zip(got, xs):
         ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
         assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+
+
+@pytest.mark.parametrize("group", ["2", "3"])
+def test_pipeline_production_groups(group, monkeypatch):
+    """H > 256 (C5-like): the recurrences of G consecutive batches run as one
+    (one per-frame MFMA step launch for all of them); a partial group is
+    produced when its results are asked for.  Same bits as one batch at a
+    time (asr_rnn_fwd + asr_linear_fwd + asr_ctc_decode)."""
+    monkeypatch.setenv("ASR_PIPELINE_GROUP", group)
+    T, B, inp, H, V, beam = 16, 16, 32, 384, 70, 12
+    W = _weights(inp, H, V, seed=int(group))
+    rng = np.random.default_rng(int(group))
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(5)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert d["mode"] == "CU groups (H > 256)" and d["groups"] == int(group), d
+    got = []
+    for i, x in enumerate(xs):
+        p.submit(x)
+        if i == 1:   # batch 0 asked for before its group is complete
+            lab, ln, lp, _ = p.collect()
+            got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    while p.pending():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    p.close()
+    assert len(got) == len(xs)
+    for g, x in zip(got, xs):
+        ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_AUTO)
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
