@@ -58,7 +58,14 @@ import numpy as np
 # 3.48 M frames/s, gpurun_out/r2g31).  Read when the HIP runtime starts.
 # Small shards (C4 at N = 8: 256 utterances per GPU) keep 8 decodes and 8
 # productions in flight: 17 streams.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+# --hw-queues N (read here, before the HIP runtime starts) measures the
+# library at another queue count, e.g. HIP's default 4.
+_hwq = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--hw-queues=")), None)
+if _hwq is None and "--hw-queues" in sys.argv[:-1]:
+    _hwq = sys.argv[sys.argv.index("--hw-queues") + 1]
+if _hwq is not None:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(_hwq))
+elif int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 try:
@@ -314,6 +321,8 @@ def launch_ranks(n: int) -> int:
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this run (default 24; the library fits its schedule to it)")
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); started by this script when WORLD_SIZE is unset")
     ap.add_argument("--steps", type=int, default=20)

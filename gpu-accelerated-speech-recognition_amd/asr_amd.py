@@ -599,14 +599,14 @@ class Pipeline:
         fz, gr, rk = _i(), ctypes.c_longlong(), _i()
         check(lib().asr_pipeline_get_production(self.h, ctypes.byref(fz), ctypes.byref(gr), ctypes.byref(rk)),
               "asr_pipeline_get_production")
-        ns, hq, sg, gr = _i(), _i(), _i(), _i()
+        ns, hq, sg, gp = _i(), _i(), _i(), _i()
         check(lib().asr_pipeline_get_streams(self.h, ctypes.byref(ns), ctypes.byref(hq)), "asr_pipeline_get_streams")
         check(lib().asr_pipeline_get_segments(self.h, ctypes.byref(sg)), "asr_pipeline_get_segments")
-        check(lib().asr_pipeline_get_groups(self.h, ctypes.byref(gr)), "asr_pipeline_get_groups")
+        check(lib().asr_pipeline_get_groups(self.h, ctypes.byref(gp)), "asr_pipeline_get_groups")
         return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
                 "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
                 "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
-                "hw_queues": hq.value, "segments": sg.value, "groups": gr.value}
+                "hw_queues": hq.value, "segments": sg.value, "groups": gp.value}
 
     def submit(self, x: "DeviceMatrix") -> None:
         """Queue a batch.  x is kept alive here until its batch is collected

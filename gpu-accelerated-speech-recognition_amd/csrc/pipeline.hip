@@ -510,10 +510,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     }
     if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
     // T-segments (fused production only): explicit, ASR_PIPELINE_SEGMENTS
-    // (A/B), else 1
+    // (A/B), else 2 for small shards (under 512 utterances: the job's fill
+    // and drain are a large part of it; measured at 256 per GPU, 20 steps:
+    // 1 / 2 / 4 segments 132.5 / 136.4 / 134.7 M frames/s), 1 otherwise
+    // (2048 per GPU: 206.7 vs 201.6 M at 2; profiles/r04/bench_scan.md)
     if (p->fuse && p->mode == SHARED) {
         const char* se = getenv("ASR_PIPELINE_SEGMENTS");
-        int S = c.segments ? c.segments : (se ? atoi(se) : 1);
+        int S = c.segments ? c.segments : (se ? atoi(se) : (c.B < 512 ? 2 : 1));
         p->S = std::max(1, std::min(S, c.T));
     }
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES

@@ -239,3 +239,35 @@ def test_pipeline_production_groups(group, monkeypatch):
     for g, x in zip(got, xs):
         ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_AUTO)
         assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+
+
+def test_pipeline_fits_hw_queues(monkeypatch):
+    """asr_pipeline_create fits its automatic schedule to GPU_MAX_HW_QUEUES
+    (streams sharing a hardware queue serialise): at HIP's default of 4 the
+    chip-filling schedule drops production streams, then the decode CUs'
+    share of the input projection; explicit counts are kept.  The results
+    are the same bits either way."""
+    T, B, inp, H, V, beam = 24, 600, 64, 256, 29, 30
+    W = _weights(inp, H, V, seed=13)
+    x = asr.DeviceMatrix.from_numpy(np.random.default_rng(2).uniform(-1, 1, (T * B, inp)).astype(np.float32))
+    full = asr.Pipeline(T, B, inp, H, V, beam, W).describe()
+    assert full["hw_queues"] == 24 and full["streams"] <= 24 and full["decode_cu_gemm_rows"] > 0, full
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert d["hw_queues"] == 4 and d["streams"] <= 4, d
+    assert d["prod_streams"] < full["prod_streams"] and d["decode_cu_gemm_rows"] == 0, (d, full)
+    for _ in range(3):
+        p.submit(x)
+    got = []
+    while p.pending():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    p.close()
+    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
+    for g in got:
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+    q = asr.Pipeline(T, B, inp, H, V, beam, W, inflight=3, prod_streams=3)   # explicit: kept
+    dq = q.describe()
+    q.close()
+    assert dq["inflight"] == 3 and dq["prod_streams"] == 3 and dq["streams"] > 4, dq
