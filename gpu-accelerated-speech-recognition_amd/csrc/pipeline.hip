@@ -545,7 +545,14 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     p->s_dec.assign(p->D, nullptr);
     p->s_prod.assign(p->P, nullptr);
     if (p->mode == SHARED) {
-        for (int d = 0; d < p->D; d++) mk(&p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
+        // ASR_PIPELINE_DGROUPS=1 (A/B): decode d on its own 1/D of the decode
+        // CUs (several rounds of utterances per CU) instead of all of them
+        static const bool dgroups = [] { const char* e = getenv("ASR_PIPELINE_DGROUPS"); return e && atoi(e); }();
+        const int dc = p->dcus ? p->dcus : ncu;
+        for (int d = 0; d < p->D; d++) {
+            if (dgroups && p->D > 1) mk(&p->s_dec[d], d * dc / p->D / 8 * 8, (d + 1) * dc / p->D / 8 * 8);
+            else mk(&p->s_dec[d], 0, dc);
+        }
         for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->dcus, ncu);
         if (p->grows > 0) mk(&p->s_gdec, 0, p->dcus);
     } else {
