@@ -845,7 +845,7 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                 lst = [r for k, v in ks.items() if k.startswith(prefix) for r in v]
                 return max(lst, key=lambda r: r["gflop"]) if lst else None
             for stage, kern in (("input_gemm", "gemm_wide_kernel"), ("emission_gemm", "gemm_narrow_kernel"),
-                                ("recurrence_emission", "rnn_recur_mfma_kernel<true>")):
+                                ("recurrence_emission", "rnn_recur_mfma_kernel<true")):
                 r = pick(kern)
                 if stage in mfma and r:
                     mfma[stage]["counters"] = {k: r[k] for k in ("mfma_busy", "cus", "gflop", "clock_ghz",

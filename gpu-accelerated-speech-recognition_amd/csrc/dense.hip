@@ -652,7 +652,9 @@ constexpr int RM_NCH = RNN_HMAX / 16;  // 16-k chunks at H = 256
 constexpr int RE_VMAX = 32;           // EMIT: vocabulary columns (two 16-column tiles)
 constexpr int RE_PART = (RNN_HMAX / 32) * RM_ROWS * RE_VMAX;   // EMIT: one buffer of 8 waves' 16 x 32 partials
 
-template <bool EMIT>
+// HL: also write h_{T-1} to hlast (segmented production); a separate
+// instance, so that the unsegmented kernel carries no extra state.
+template <bool EMIT, bool HL = false>
 __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __restrict__ h0,
                                                              const float* __restrict__ Whh,
                                                              const float* __restrict__ b_ih,
@@ -864,7 +866,7 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
         cur ^= 1;
         lds_barrier();
     }
-    if (hlast) {   // h_{T-1} of this workgroup's rows (may be h0's buffer: every row is read above)
+    if (HL && hlast) {   // h_{T-1} of this workgroup's rows (may be h0's buffer: every row is read above)
         for (int x = tid; x < RM_ROWS * H; x += nthr) {
             const int r = x / H, k = x - r * H;
             if (r0 + r < B) hlast[(long)(r0 + r) * H + k] = hs[cur][r * RM_LD + k];
@@ -896,9 +898,14 @@ int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, c
                          int T, int B, int H, int V, hipStream_t s, float* hlast) {
     if (H > RNN_HMAX || (H & 15) != 0 || B <= 0 || V < 1 || V > RE_VMAX) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
-    hipLaunchKernelGGL(rnn_recur_mfma_kernel<true>, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
-                       dim3(64 * ((H / 16 + 1) / 2)), 0, s,
-                       h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H, V, hlast);
+    if (hlast)
+        hipLaunchKernelGGL((rnn_recur_mfma_kernel<true, true>), dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
+                           dim3(64 * ((H / 16 + 1) / 2)), 0, s,
+                           h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H, V, hlast);
+    else
+        hipLaunchKernelGGL((rnn_recur_mfma_kernel<true, false>), dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
+                           dim3(64 * ((H / 16 + 1) / 2)), 0, s,
+                           h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H, V, nullptr);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }
