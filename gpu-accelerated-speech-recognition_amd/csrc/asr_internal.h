@@ -36,6 +36,10 @@ extern thread_local int asr_internal_rnn_kind;
 // kernel (short-lived workgroups) instead of the persistent wide one, so that
 // a decode launched meanwhile waits at most one tile for its CUs.  Same bits.
 extern thread_local int asr_internal_gemm_tiled;
+// Set by the pipeline around its productions: capture the per-frame
+// recurrence launches (H > 256) into the library's HIP graph at their first
+// use, not the second (a pipeline's buffers recur; one-off calls stay eager).
+extern thread_local int asr_internal_graph_now;
 // One-wave decoder workgroups (utterances) that fit on one CU for this
 // handle's layout (the occupancy query); 0 when the one-wave kernel does not
 // apply (V > 63, .cu semantics, timesteps).  For the pipeline's schedule.

@@ -140,7 +140,9 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
     asr_internal_rnn_kind = p->rnn_kind;
+    asr_internal_graph_now = 1;
     int rc = asr_rnn_fwd(x, nullptr, p->W_ih, p->W_hh, p->b_ih, p->b_hh, p->hid[k], c.T, c.B, c.in, c.H, sp);
+    asr_internal_graph_now = 0;
     asr_internal_rnn_kind = -1;
     if (!rc) rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
                                  ASR_EPI_BIAS_LOGSOFTMAX, sp);
@@ -310,7 +312,9 @@ int flush_group(asr_pipeline* p) {
     hipStream_t sp = p->s_prod[(g[0] / p->G) % p->P];
     float* hids[4];
     for (size_t j = 0; j < g.size(); j++) hids[j] = p->hid[g[j] % p->nbuf];
+    asr_internal_graph_now = 1;
     int rc = asr_internal_rnn_recur_multi(p->W_hh, p->b_ih, p->b_hh, hids, (int)g.size(), c.T, c.B, c.H, sp);
+    asr_internal_graph_now = 0;
     for (size_t j = 0; j < g.size() && !rc; j++) {
         const int k = (int)(g[j] % p->nbuf);
         rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
@@ -343,8 +347,11 @@ int flush_tail(asr_pipeline* p) {
 }
 
 // Fetch the results of the oldest uncollected batch (blocking).
-int fetch(asr_pipeline* p, Result& r) {
-    const auto& c = p->cfg;
+// ... straight into the caller's arrays (asr_ctc_get_best's layout): the
+// host copies of a batch's results are on the critical path of small
+// batches (C2: 0.6 ms per batch), so nothing is staged in between.
+int fetch_to(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, double* logp, float* ms, long* batch,
+             int* res_rc) {
     const long j = p->collected;
     if (j >= p->submitted) return ASR_ERR_STATE;
     if (p->fail_from >= 0 && j >= p->fail_from) return p->fail_rc;
@@ -355,15 +362,22 @@ int fetch(asr_pipeline* p, Result& r) {
     }
     if (j >= p->decoded) return ASR_ERR_INTERNAL;   // never queued (cannot happen once flushed)
     asr_ctc_t* h = p->dec[j % p->nbuf];
+    *res_rc = asr_ctc_get_best(h, labels, max_len, lengths, logp);
+    if (*res_rc != ASR_OK && *res_rc != ASR_ERR_BEAM_OVERFLOW) return *res_rc;
+    if (ms) asr_ctc_last_kernel_ms(h, ms);
+    *batch = j;
+    p->collected = j + 1;
+    return ASR_OK;
+}
+
+// Fetch the results of the oldest uncollected batch into a stash entry (a
+// submit that must reuse its buffer before the caller collected it).
+int fetch(asr_pipeline* p, Result& r) {
+    const auto& c = p->cfg;
     r.lab.assign((size_t)c.B * c.T, 0);
     r.len.assign(c.B, 0);
     r.lp.assign(c.B, 0.0);
-    r.rc = asr_ctc_get_best(h, r.lab.data(), c.T, r.len.data(), r.lp.data());
-    if (r.rc != ASR_OK && r.rc != ASR_ERR_BEAM_OVERFLOW) return r.rc;
-    asr_ctc_last_kernel_ms(h, &r.ms);
-    r.batch = j;
-    p->collected = j + 1;
-    return ASR_OK;
+    return fetch_to(p, r.lab.data(), c.T, r.len.data(), r.lp.data(), &r.ms, &r.batch, &r.rc);
 }
 
 void release(asr_pipeline* p) {
@@ -545,14 +559,10 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     p->s_dec.assign(p->D, nullptr);
     p->s_prod.assign(p->P, nullptr);
     if (p->mode == SHARED) {
-        // ASR_PIPELINE_DGROUPS=1 (A/B): decode d on its own 1/D of the decode
-        // CUs (several rounds of utterances per CU) instead of all of them
-        static const bool dgroups = [] { const char* e = getenv("ASR_PIPELINE_DGROUPS"); return e && atoi(e); }();
-        const int dc = p->dcus ? p->dcus : ncu;
-        for (int d = 0; d < p->D; d++) {
-            if (dgroups && p->D > 1) mk(&p->s_dec[d], d * dc / p->D / 8 * 8, (d + 1) * dc / p->D / 8 * 8);
-            else mk(&p->s_dec[d], 0, dc);
-        }
+        // every decode on all of the decode CUs (decode d on its own 1/D of
+        // them, several rounds of utterances per CU: 206.7 -> 196.9 M frames/s
+        // at C4, D = 2, profiles/r04/bench_scan.md)
+        for (int d = 0; d < p->D; d++) mk(&p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
         for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->dcus, ncu);
         if (p->grows > 0) mk(&p->s_gdec, 0, p->dcus);
     } else {
@@ -662,14 +672,16 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
 int asr_pipeline_collect(asr_pipeline_t* p, int32_t* labels, int max_len, int32_t* lengths, double* logp,
                          float* decode_ms) {
     if (!p || (!labels && max_len > 0)) return ASR_ERR_ARG;
-    Result r;
-    if (!p->stash.empty()) {
-        r = std::move(p->stash.front());
-        p->stash.pop_front();
-    } else {
-        int rc = fetch(p, r);
+    if (p->stash.empty()) {   // the common case: straight into the caller's arrays
+        long batch = -1;
+        int res = ASR_OK;
+        const int rc = fetch_to(p, labels, max_len, lengths, logp, decode_ms, &batch, &res);
         if (rc) return rc;
+        p->returned = batch;
+        return res;
     }
+    Result r = std::move(p->stash.front());
+    p->stash.pop_front();
     const auto& c = p->cfg;
     for (int b = 0; b < c.B; b++) {
         const int len = r.len[b];

@@ -20,6 +20,7 @@ thread_local std::string g_last_error;
 }
 
 thread_local int asr_internal_rnn_kind = -1;
+thread_local int asr_internal_graph_now = 0;
 thread_local int asr_internal_gemm_tiled = 0;
 
 void asr_internal_set_error(const char* what, const char* msg, const char* file, int line) {
@@ -266,7 +267,7 @@ static int rnn_recurrence_frames(const float* h0, const float* W_hh, const float
         e = &g_graphs.back();
     }
     e->last = ++g_graph_tick;
-    if (++e->uses < 2 && !e->exec)   // first use: eager (kernel attributes set, nothing captured for one-offs)
+    if (++e->uses < 2 && !e->exec && !asr_internal_graph_now)   // first use: eager (nothing captured for one-offs)
         return rnn_frames_eager(h0, W_hh, b_ih, b_hh, hids, nb, T, B, H, st);
     if (!e->exec) {
         hipStream_t cs;
@@ -1074,7 +1075,7 @@ int asr_ctc_get_best(asr_ctc_t* h, int32_t* labels, int max_len, int32_t* length
         if (labels) {
             const int* fwd = h->h_best_lab + (size_t)b * pitch;
             const int n = std::min(len, max_len);
-            for (int i = 0; i < n; i++) labels[(size_t)b * max_len + i] = fwd[i];
+            if (n > 0) std::memcpy(labels + (size_t)b * max_len, fwd, sizeof(int) * (size_t)n);
         }
     }
     return stc;
