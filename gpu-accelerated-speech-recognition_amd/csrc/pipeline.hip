@@ -355,7 +355,16 @@ int fetch_to(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, do
     const long j = p->collected;
     if (j >= p->submitted) return ASR_ERR_STATE;
     if (p->fail_from >= 0 && j >= p->fail_from) return p->fail_rc;
-    if (j >= p->decoded) {
+    // Work held back for overlap (a split production's last emission GEMM +
+    // decode, a production group still filling) is queued before the host
+    // blocks on a batch within D of it: the caller is draining (no submit
+    // comes while it waits), and held back it would start only when the
+    // caller reaches it (C2, 20 steps: the last decode started 1.5 ms late,
+    // 8 % of the job).  In steady state the caller fetches batches more than
+    // D behind the newest, so nothing changes there.
+    const bool drain_tail = p->pending_tail >= 0 && j + p->D >= p->pending_tail;
+    const bool drain_group = !p->group.empty() && j + p->D >= p->group.front();
+    if (j >= p->decoded || drain_tail || drain_group) {
         int rc = flush_tail(p);
         if (!rc) rc = flush_group(p);
         if (rc) return rc;
@@ -460,9 +469,11 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // CUs 137-142 / 155-162 / 145 M frames/s; at 512: 128 / 96 CUs
         // 183 / 168-182 M; profiles/r03/bench_scan.md).  Beam capacity
         // 65-128 (C3's beam 100: two rows per lane): an utterance-frame costs
-        // the decoder ~4x the CU time (0.49 vs 2.0 utterance-frames per us
-        // per CU), the production the same, so 3/4 of the CUs decode.
-        const int dauto = (kcap > 64 ? ncu * 3 / 4 : (c.B < 512 ? ncu * 3 / 8 : ncu / 2)) / 8 * 8;
+        // the decoder more CU time, so half of them decode at any batch size
+        // (C3, B = 256, 20 steps: 96 / 112 / 128 / 144 / 160 / 176 / 192
+        // decode CUs 59.5 / 72.5 / 88.3 / 79.4 / 77.1 / 57.2 / 61.1 M frames/s,
+        // profiles/r04/bench_scan.md).
+        const int dauto = (kcap > 64 ? ncu / 2 : (c.B < 512 ? ncu * 3 / 8 : ncu / 2)) / 8 * 8;
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : dauto) : 0;
         const int dc = p->dcus ? p->dcus : ncu;
         // as many batches decoding at once as fill the decode CUs at the
