@@ -25,9 +25,10 @@
 //           with the emission projection fused (asr_rnn_emit_fwd, V <= 32),
 //           part of the input projection optionally on the decode CUs.
 //   GROUPS2 H > 256 (C5: 2000 per-frame recurrence launches, replayed from
-//           the library's HIP graph): the recurrences of G = 2 consecutive
-//           batches run as one (production groups), D = 2G decode groups,
-//           2 production streams on the remaining CUs.
+//           the library's HIP graph): D = 2 decode groups, 2 production
+//           streams on the remaining CUs; optionally the recurrences of G
+//           consecutive batches as one (production groups, measured slower
+//           at C5, off by default).
 // Results come back in submission order (asr_pipeline_collect).  A batch's
 // buffers are reused only after its results were fetched (the decoder's
 // overflow retry re-reads its emissions): submit collects internally when
@@ -509,11 +510,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->mode = GROUPS2;
         p->gcu = bcu;
         // production groups: G batches' recurrences as one (H > 256, the
-        // per-frame step launches; rows in whole 16-row tiles), default 2
-        // (ASR_PIPELINE_GROUP: A/B).  A step of 2 batches costs about one,
-        // so production keeps up with ~2x the decodes: D = 2G.
+        // per-frame step launches; rows in whole 16-row tiles), D = 2G.
+        // Default 1 (ASR_PIPELINE_GROUP=n selects n): measured at C5, a
+        // 64-row step beside the production GEMMs costs 2.1x a 32-row one
+        // (14.9 vs 6.9 us), so groups of 2 / 3 ran 1.77 / 1.45 M frames/s
+        // against 3.37 M (profiles/r04/bench_scan.md).
         const char* ge = getenv("ASR_PIPELINE_GROUP");
-        const int Gw = ge ? atoi(ge) : 2;
+        const int Gw = ge ? atoi(ge) : 1;
         p->G = (c.H > 256 && (c.H % 128) == 0 && (c.B % 16) == 0) ? std::max(1, std::min(4, Gw)) : 1;
         p->D = c.inflight ? c.inflight : std::max(1, std::min(2 * p->G, ncu / bcu - 1));
         p->P = c.prod_streams ? c.prod_streams : (c.H > 256 ? 2 : 1);
