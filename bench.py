@@ -82,6 +82,8 @@ from __graft_entry__ import PKG, _load  # noqa: E402
 METRIC = "frames/sec decoded (RNN+CTC beam) at beam=50, vocab=29; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TF = 157.3  # dense fp32 MFMA = fp32 vector peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TF = 2516.6  # dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz (~2.5 PF)
+SPLIT_PRODUCTS = 6          # bf16 MFMA products per fp32 product on the split arithmetic (dense_x3.hip)
 
 # BASELINE.json configs: T, utterances per GPU, hidden, vocab, beam.
 CONFIGS = {
@@ -844,8 +846,11 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
             def pick(prefix, biggest=True):
                 lst = [r for k, v in ks.items() if k.startswith(prefix) for r in v]
                 return max(lst, key=lambda r: r["gflop"]) if lst else None
-            for stage, kern in (("input_gemm", "gemm_wide_kernel"), ("emission_gemm", "gemm_narrow_kernel"),
-                                ("recurrence_emission", "rnn_recur_mfma_kernel<true")):
+            split = mfma.get("arith") == "split_bf16"
+            for stage, kern in (("input_gemm", "gemm_x3_kernel<" if split else "gemm_wide_kernel"),
+                                ("emission_gemm", "gemm_narrow_kernel"),
+                                ("recurrence_emission",
+                                 "rnn_recur_x3_kernel<8,true" if split else "rnn_recur_mfma_kernel<true")):
                 r = pick(kern)
                 if stage in mfma and r:
                     mfma[stage]["counters"] = {k: r[k] for k in ("mfma_busy", "cus", "gflop", "clock_ghz",
@@ -870,7 +875,9 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
-            "dtype": "f32 (RNN/Linear MFMA) + f64 (beam scores)",
+            "dtype": ("f32 (RNN/Linear: fp32-accurate split-bf16 MFMA, x = h + m + l, 6 products) + f64 "
+                      "(beam scores)" if asr.get_dense_arith() == asr.DENSE_SPLIT_BF16
+                      else "f32 (RNN/Linear fp32 MFMA) + f64 (beam scores)"),
             "data": "synthetic: U(-1,1) features from numpy PCG64 seeded per utterance "
                     "(20261016+u), random-init weights (PCG64 20261015); emissions = "
                     "log_softmax of the RNN->Linear output (not SURVEY §8(d)'s mt19937_64 "
@@ -880,6 +887,7 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                        "batch_per_gpu": B, "global_batch": GB, "T": T, "hidden": H,
                        "vocab": V, "beam": beam, "parallelism": f"utterance-shard x{world}",
                        "decode_waves": dec_config[1],   # the schedule the decodes ran
+                       "dense_arith": "split_bf16" if asr.get_dense_arith() == asr.DENSE_SPLIT_BF16 else "f32",
                        **sched},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "parity": parity, "gather": gather,
         }
@@ -1135,7 +1143,11 @@ def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V
     whole chip, so its utilisation is that of ceil(B / 16) CUs' worth of work
     spread over the launch time)."""
     st = torch.cuda.current_stream()
-    out = {}
+    split = asr.get_dense_arith() == asr.DENSE_SPLIT_BF16
+    out = {"arith": "split_bf16" if split else "f32",
+           "note": "tflops = fp32 FLOP / s against the fp32 MFMA peak (mfma_util); on the split "
+                   "arithmetic each fp32 product is 6 bf16 MFMA products (bf16_mfma_util against "
+                   "the dense bf16 peak)" if split else "tflops = fp32 FLOP / s against the fp32 MFMA peak"}
     stages = [
         ("input_gemm", lambda: asr.linear_fwd(d_x, d_wih, None, d_hid, asr.EPI_NONE, st.cuda_stream),
          2.0 * T * B * In * H),
@@ -1160,6 +1172,9 @@ def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V
         out[name] = {"us": round(us, 2), "tflops": round(tf, 2),
                      "mfma_util": round(tf / FP32_MFMA_PEAK_TF, 4),
                      "hbm_gbs": round(hbm / (us * 1e-6) / 1e9, 1)}
+        if split and name != "emission_gemm":   # fp32 work on the bf16 matrix cores, 6 products each
+            out[name]["bf16_mfma_tflops"] = round(SPLIT_PRODUCTS * tf, 1)
+            out[name]["bf16_mfma_util"] = round(SPLIT_PRODUCTS * tf / BF16_MFMA_PEAK_TF, 4)
         if name == "recurrence_emission":   # per busy CU: one 16-utterance workgroup per CU
             busy = min(-(-B // 16), torch.cuda.get_device_properties(st.device).multi_processor_count)
             ncu = torch.cuda.get_device_properties(st.device).multi_processor_count

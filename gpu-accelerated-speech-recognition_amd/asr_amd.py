@@ -56,6 +56,7 @@ EXPORTS = [
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_decode_segment", "asr_ctc_set_semantics",
     "asr_ctc_set_timesteps", "asr_ctc_get_beams_ts", "asr_ctc_set_result_stream",
     "asr_ctc_set_concurrency", "asr_rnn_set_recurrence", "asr_rnn_get_recurrence",
+    "asr_set_dense_arith", "asr_get_dense_arith",
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
     "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams",
     "asr_pipeline_peek_emissions", "asr_pipeline_get_segments", "asr_pipeline_get_groups",
@@ -114,6 +115,8 @@ def lib() -> ctypes.CDLL:
         "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_set_recurrence": [_i],
         "asr_rnn_get_recurrence": [ctypes.POINTER(_i)],
+        "asr_set_dense_arith": [_i],
+        "asr_get_dense_arith": [ctypes.POINTER(_i)],
         "asr_rnn_emit_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_pipeline_create": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)],
         "asr_pipeline_submit": [_vp, _vp],
@@ -316,6 +319,21 @@ def rnn_get_recurrence() -> int:
     k = _i()
     check(lib().asr_rnn_get_recurrence(ctypes.byref(k)), "asr_rnn_get_recurrence")
     return k.value
+
+
+DENSE_F32, DENSE_SPLIT_BF16 = 0, 1
+
+
+def set_dense_arith(arith: int) -> None:
+    """Process-wide arithmetic of the dense contractions (asr_set_dense_arith):
+    DENSE_SPLIT_BF16 (default, fp32-accurate three-piece bf16 MFMA) or DENSE_F32."""
+    check(lib().asr_set_dense_arith(int(arith)), "asr_set_dense_arith")
+
+
+def get_dense_arith() -> int:
+    a = _i()
+    check(lib().asr_get_dense_arith(ctypes.byref(a)), "asr_get_dense_arith")
+    return a.value
 
 
 def rnn_cell_fwd(x: DeviceMatrix, h_prev: DeviceMatrix, W_ih: DeviceMatrix,

@@ -52,6 +52,22 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                     const float* b_hh, int B, int H, hipStream_t s);
 
+// Split-bf16 arithmetic (dense_x3.hip): fp32-accurate products on the bf16
+// matrix cores.  The setting (asr_set_dense_arith) picks it for every shape
+// below that it applies to; the fp32 kernels otherwise.
+int dense_arith();
+void dense_arith_set(int a);
+bool dense_x3_on();
+bool gemm_x3_applies(const GemmArgs& g, int epi);
+// tpw > 0: runs of tpw 16-row tiles per workgroup (short workgroups); 0: persistent.
+int gemm_x3_launch(const GemmArgs& g, int epi, int tpw, hipStream_t s);
+bool rnn_x3_applies(int B, int H);
+int rnn_recur_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                        int T, int B, int H, hipStream_t s);
+int rnn_emit_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, const float* P,
+                       float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int H, int V,
+                       hipStream_t s, float* hlast);
+
 // Bidirectional RNN plumbing (H % 4 == 0, 16-B aligned buffers).
 int time_reverse_launch(float* p, int T, long n, hipStream_t s);
 int bidir_concat_launch(const float* hf, const float* hr, float* out, int T, int B, int H,

@@ -467,6 +467,10 @@ static int launch_gemm_epi(const GemmArgs& g, hipStream_t s) {
 
 int gemm_launch(const GemmArgs& g, int epi, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return ASR_ERR_ARG;
+    // fp32-accurate split-bf16 kernel (dense_x3.hip) for the shapes it takes;
+    // the pipeline's short-workgroup request (asr_internal_gemm_tiled) runs it
+    // in 8-tile runs instead of persistent workgroups
+    if (dense_x3_on() && gemm_x3_applies(g, epi)) return gemm_x3_launch(g, epi, asr_internal_gemm_tiled ? 8 : 0, s);
     if (epi == EPI_LOGSOFTMAX && g.N > 64) {
         // Rows wider than one workgroup tile (e.g. C5's V = 1000): bias GEMM,
         // then a row-wise log_softmax pass in place (model.py:49).
@@ -884,6 +888,7 @@ __global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __rest
 
 int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                           float* hid, int T, int B, int H, hipStream_t s) {
+    if (dense_x3_on() && rnn_x3_applies(B, H)) return rnn_recur_x3_launch(h0, Whh, b_ih, b_hh, hid, T, B, H, s);
     if (H > RNN_HMAX || (H & 15) != 0 || B <= 0) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
     hipLaunchKernelGGL(rnn_recur_mfma_kernel<false>, dim3((unsigned)((B + RM_ROWS - 1) / RM_ROWS)),
@@ -896,6 +901,8 @@ int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, 
 int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                          const float* P, float* hout, const float* Wout, const float* bout, float* emis,
                          int T, int B, int H, int V, hipStream_t s, float* hlast) {
+    if (dense_x3_on() && rnn_x3_applies(B, H) && V >= 1 && V <= RE_VMAX)
+        return rnn_emit_x3_launch(h0, Whh, b_ih, b_hh, P, hout, Wout, bout, emis, T, B, H, V, s, hlast);
     if (H > RNN_HMAX || (H & 15) != 0 || B <= 0 || V < 1 || V > RE_VMAX) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
     if (hlast)

@@ -1,0 +1,593 @@
+// ============================================================================
+// fp32-accurate dense kernels on the bf16 matrix cores (gfx950).
+//
+// Every fp32 operand x is split into three bf16 pieces, x = h + m + l:
+// h = bf16(x), m = bf16(x - h), l = bf16(x - h - m), each rounded to nearest;
+// the two subtractions are exact in fp32, and l captures the remainder exactly
+// (24 bits = 8 + 8 + 8), so h + m + l == x.  A product x.y keeps the six
+// piece products of order >= 2^-18 (hh, hm, mh, hl, mm, lh), each exact in
+// fp32 (8 x 8 significant bits), accumulated by the MFMA in fp32; the three
+// dropped ones (ml, lm, ll) are below 2^-25 |x.y|.  The result is as accurate
+// as an fp32 GEMM (measured against fp64: max error / sum|x.y| 2.2e-7 vs
+// 3.3e-7 for a sequential fp32 FMA chain, tools/x3_probe.hip) — a rounding
+// difference, not a precision reduction.  Six v_mfma_f32_16x16x32_bf16 (16
+// cycles each per SIMD) do the work of 8 v_mfma_f32_16x16x4_f32 (32 cycles):
+// 2.7x the fp32 MFMA rate.
+//
+// The same shapes run on the fp32 kernels of dense.hip when the split
+// arithmetic is off (asr_set_dense_arith(ASR_DENSE_F32)); the choice depends on
+// the shape and that setting only, never on M or on the grid, so a row's bits
+// do not depend on the batch it is in (utterance sharding relies on that).
+// ============================================================================
+#include "dense.h"
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+
+namespace asr {
+
+// ASR_DENSE_F32 / ASR_DENSE_SPLIT_BF16 (asr_set_dense_arith); initial value
+// from ASR_DENSE ("f32" / "x3"), else the split arithmetic.
+static std::atomic<int> g_dense_arith{-1};
+int dense_arith() {
+    int a = g_dense_arith.load(std::memory_order_relaxed);
+    if (a < 0) {
+        const char* e = getenv("ASR_DENSE");
+        a = (e && !strcmp(e, "f32")) ? ASR_DENSE_F32 : ASR_DENSE_SPLIT_BF16;
+        int expect = -1;
+        g_dense_arith.compare_exchange_strong(expect, a);
+        a = g_dense_arith.load(std::memory_order_relaxed);
+    }
+    return a;
+}
+void dense_arith_set(int a) { g_dense_arith.store(a, std::memory_order_relaxed); }
+bool dense_x3_on() { return dense_arith() == ASR_DENSE_SPLIT_BF16; }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+// raw buffer resources: loads past num_records return 0, stores are dropped
+// (the row tails of a tile / a step need no branches)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, long bytes) {
+    const int n = bytes < 0x7fffffffL ? (int)bytes : 0x7fffffff;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
+// acc[ct] += A . B over one 32-k chunk for NT column tiles, the six piece
+// products in ascending order of magnitude; consecutive MFMAs go to different
+// accumulators (independent chains).
+#define X3_PRODUCTS(NT, ACC, AH, AM, AL, BH, BM, BL, C)                                           \
+    {                                                                                             \
+        _Pragma("unroll") for (int ct_ = 0; ct_ < NT; ct_++) ACC[ct_] =                           \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(AL, BH[ct_][C], ACC[ct_], 0, 0, 0);           \
+        _Pragma("unroll") for (int ct_ = 0; ct_ < NT; ct_++) ACC[ct_] =                           \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(AM, BM[ct_][C], ACC[ct_], 0, 0, 0);           \
+        _Pragma("unroll") for (int ct_ = 0; ct_ < NT; ct_++) ACC[ct_] =                           \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(AH, BL[ct_][C], ACC[ct_], 0, 0, 0);           \
+        _Pragma("unroll") for (int ct_ = 0; ct_ < NT; ct_++) ACC[ct_] =                           \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(AM, BH[ct_][C], ACC[ct_], 0, 0, 0);           \
+        _Pragma("unroll") for (int ct_ = 0; ct_ < NT; ct_++) ACC[ct_] =                           \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(AH, BM[ct_][C], ACC[ct_], 0, 0, 0);           \
+        _Pragma("unroll") for (int ct_ = 0; ct_ < NT; ct_++) ACC[ct_] =                           \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(AH, BH[ct_][C], ACC[ct_], 0, 0, 0);           \
+    }
+
+__device__ __forceinline__ void lds_barrier_x3() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// ---------------------------------------------------------------------------
+// GEMM C = A.B (+ bias, ReLU), K <= 256, any N (256 columns per workgroup
+// row of the grid): the RNN input projection (cuMatrix.cpp:33-70 /
+// RNN.cu:9-30's x.W_ih) and the Linear layers (Linear.cu:3-10).
+//   * 8 waves, two per SIMD (one wave's VALU issues beside the other's
+//     MFMAs); wave w owns columns n0 + 32w .. + 31 as two 16-column tiles and
+//     keeps their B pieces in registers for the whole launch (2 x NCH x 3
+//     bf16x8 = 24 NCH registers).
+//   * 16-row tiles of A: staged once per tile to LDS as the three pieces
+//     (double-buffered, one barrier per tile), the next tile's A in flight
+//     during this tile's MFMAs; the A fragment of MFMA (chunk c) is one
+//     ds_read_b128 per piece (row c15, k = 32c + 8g .. + 7).
+//   * Row tiles per workgroup: tpw > 0 a contiguous run of tpw tiles (short
+//     workgroups that free their CU soon), 0 persistent (stride gridDim.x).
+// ---------------------------------------------------------------------------
+constexpr int X3_ROWS = 16;
+constexpr int X3_WAVES = 8;
+constexpr int X3_NCOL = 32 * X3_WAVES;
+
+template <int NCH>
+constexpr int x3_gemm_lds() {
+    return 2 * 3 * X3_ROWS * (NCH * 32 + 8) * 2;
+}
+
+template <int NCH, int EPI>
+__global__ __launch_bounds__(64 * X3_WAVES) void gemm_x3_kernel(GemmArgs g, int tpw) {
+    constexpr int KC = NCH * 32;              // staged k columns (zero past K)
+    constexpr int AS = KC + 8;                // LDS row stride (bf16): rows 16 B apart in banks
+    constexpr int PIECE = X3_ROWS * AS;
+    constexpr int NV4 = X3_ROWS * KC / 4;     // float4 per tile
+    constexpr int NL = (NV4 + 64 * X3_WAVES - 1) / (64 * X3_WAVES);
+    extern __shared__ __attribute__((aligned(16))) __bf16 x3s[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c15 = lane & 15, gq = lane >> 4;
+    const int n0 = blockIdx.y * X3_NCOL;
+    bf16x8 bh[2][NCH], bm[2][NCH], bl[2][NCH];
+    int ncol[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        const int n = n0 + 32 * w + 16 * ct + c15;
+        ncol[ct] = n;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = 32 * c + 8 * gq + j;
+                const float b = (k < g.K && n < g.N) ? g.B[(long)k * g.sbk + (long)n * g.sbn] : 0.f;
+                __bf16 h, m, l;
+                split3(b, h, m, l);
+                bh[ct][c][j] = h;
+                bm[ct][c][j] = m;
+                bl[ct][c][j] = l;
+            }
+    }
+    float bias[2] = {0.f, 0.f};
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) bias[ct] = ncol[ct] < g.N ? g.b1[ncol[ct]] : 0.f;
+    }
+    const int ntile = (g.M + X3_ROWS - 1) / X3_ROWS;
+    int tile, tend, tstep;
+    if (tpw > 0) {
+        tile = blockIdx.x * tpw;
+        tend = min(ntile, tile + tpw);
+        tstep = 1;
+    } else {
+        tile = blockIdx.x;
+        tend = ntile;
+        tstep = gridDim.x;
+    }
+    f32x4 st[NL];
+    auto load = [&](int tl) {
+        const long r0 = (long)tl * X3_ROWS;
+        const long rows = tl < tend ? min((long)X3_ROWS, (long)g.M - r0) : 0;
+        const auto rs = brsrc(g.A + r0 * g.sam, rows * g.sam * 4);
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int idx = tid + 64 * X3_WAVES * i;
+            const int row = idx / (KC / 4), k = (idx % (KC / 4)) * 4;
+            f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (row * (int)g.sam + k) * 4, 0, 0));
+            if (k >= g.K || idx >= NV4) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            st[i] = v;
+        }
+    };
+    auto stage = [&](int buf) {
+        __bf16* base = x3s + buf * 3 * PIECE;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int idx = tid + 64 * X3_WAVES * i;
+            if (NV4 % (64 * X3_WAVES) != 0 && idx >= NV4) continue;
+            const int row = idx / (KC / 4), k = (idx % (KC / 4)) * 4;
+            bf16x4 h, m, l;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                __bf16 a, b, c;
+                split3(st[i][e], a, b, c);
+                h[e] = a;
+                m[e] = b;
+                l[e] = c;
+            }
+            __bf16* p = base + row * AS + k;
+            *reinterpret_cast<bf16x4*>(p) = h;
+            *reinterpret_cast<bf16x4*>(p + PIECE) = m;
+            *reinterpret_cast<bf16x4*>(p + 2 * PIECE) = l;
+        }
+    };
+    load(tile);
+    stage(0);
+    load(tile + tstep);
+    __syncthreads();
+    int cur = 0;
+    for (; tile < tend; tile += tstep) {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const __bf16* pb = x3s + cur * 3 * PIECE;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int off = c15 * AS + 32 * c + 8 * gq;
+            const bf16x8 ah = *reinterpret_cast<const bf16x8*>(pb + off);
+            const bf16x8 am = *reinterpret_cast<const bf16x8*>(pb + PIECE + off);
+            const bf16x8 al = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
+            X3_PRODUCTS(2, acc, ah, am, al, bh, bm, bl, c)
+        }
+        stage(cur ^ 1);
+        load(tile + 2 * tstep);
+        const long r0 = (long)tile * X3_ROWS;
+        const auto cs = brsrc(g.C + r0 * g.ldc, min((long)X3_ROWS, (long)g.M - r0) * g.ldc * 4);
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            if (ncol[ct] < g.N) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float y = acc[ct][j];
+                    if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) y = y + bias[ct];
+                    if (EPI == EPI_BIAS_RELU && y < 0.f) y = 0.f;
+                    bstore(cs, ((4 * gq + j) * (int)g.ldc + ncol[ct]) * 4, y);
+                }
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+}
+
+template <int NCH, int EPI>
+static int launch_gemm_x3_k(const GemmArgs& g, int tpw, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        ASR_HIP_TRY(hipFuncSetAttribute((const void*)gemm_x3_kernel<NCH, EPI>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, x3_gemm_lds<NCH>()));
+        attr = true;
+    }
+    const int ntile = (g.M + X3_ROWS - 1) / X3_ROWS;
+    const int ncol = (g.N + X3_NCOL - 1) / X3_NCOL;
+    int rows;
+    if (tpw > 0) {
+        rows = (ntile + tpw - 1) / tpw;
+    } else {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        rows = max(1, min(ntile, ncu / max(1, ncol)));   // one workgroup per CU (2 waves per SIMD)
+    }
+    hipLaunchKernelGGL((gemm_x3_kernel<NCH, EPI>), dim3((unsigned)rows, (unsigned)ncol), dim3(64 * X3_WAVES),
+                       x3_gemm_lds<NCH>(), s, g, tpw);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+template <int EPI>
+static int launch_gemm_x3_epi(const GemmArgs& g, int tpw, hipStream_t s) {
+    if (g.K <= 32) return launch_gemm_x3_k<1, EPI>(g, tpw, s);
+    if (g.K <= 64) return launch_gemm_x3_k<2, EPI>(g, tpw, s);
+    if (g.K <= 128) return launch_gemm_x3_k<4, EPI>(g, tpw, s);
+    return launch_gemm_x3_k<8, EPI>(g, tpw, s);
+}
+
+bool gemm_x3_applies(const GemmArgs& g, int epi) {
+    if (epi != EPI_NONE && epi != EPI_BIAS && epi != EPI_BIAS_RELU) return false;
+    const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
+    return va && g.K <= 256 && g.N >= 64 && (long)g.sam * 4 * X3_ROWS < 0x7fffffffL &&
+           (long)g.ldc * 4 * X3_ROWS < 0x7fffffffL;
+}
+
+int gemm_x3_launch(const GemmArgs& g, int epi, int tpw, hipStream_t s) {
+    if (!gemm_x3_applies(g, epi)) return ASR_ERR_UNSUPPORTED;
+    switch (epi) {
+        case EPI_NONE: return launch_gemm_x3_epi<EPI_NONE>(g, tpw, s);
+        case EPI_BIAS: return launch_gemm_x3_epi<EPI_BIAS>(g, tpw, s);
+        default: return launch_gemm_x3_epi<EPI_BIAS_RELU>(g, tpw, s);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// RNN recurrence h_t = tanh((P_t + h_{t-1}.W_hh) + (b_hh + b_ih)) (the op
+// order of RNN_Cell.cu:10-12) on the split arithmetic, 16 utterances per
+// workgroup, H = 32 NCH (64, 128, 256): the fp32 rnn_recur_mfma_kernel's
+// schedule (dense.hip) with
+//   * NCH waves, wave w owning columns 32w .. 32w + 31: its W_hh pieces in
+//     registers for the whole sequence (24 NCH registers);
+//   * h_{t-1} as its three pieces in LDS, double-buffered (one barrier per
+//     step); each lane splits the h values it produces (a lane's 8 values:
+//     rows 4g + j, two columns);
+//   * P_{t+1} and the stores of h_t as buffer ops on a per-step resource
+//     (rows past B: loads read 0, stores dropped).
+// EMIT (V <= 32): the emission projection + log_softmax fused as in the fp32
+// kernel, after each step's h_t epilogue (its registers are free then): wave
+// w contracts k-chunk w of h_{t-1} with the W_out pieces of that
+// chunk (staged once in LDS in fragment order: 6 ds_read_b128 per step) into
+// a 16 x 32 partial; one step later waves 0-3 sum the partials in wave order,
+// add b_out and log-softmax each row (DPP over the 16 lanes of a row).
+// HL: also write h_{T-1} (exact: h + m + l == h) to hlast.
+// ---------------------------------------------------------------------------
+constexpr int RX_VMAX = 32;
+
+template <int NCH, bool EMIT>
+constexpr int x3_recur_lds() {
+    return 2 * 3 * 16 * (NCH * 32 + 8) * 2 + (EMIT ? 3 * NCH * 2 * 64 * 16 + 2 * NCH * 4 * 64 * 8 : 0);
+}
+
+template <int NCH, bool EMIT, bool HL>
+__global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* __restrict__ h0,
+                                                                const float* __restrict__ Whh,
+                                                                const float* __restrict__ b_ih,
+                                                                const float* __restrict__ b_hh, float* hid,
+                                                                float* hout, const float* __restrict__ Wout,
+                                                                const float* __restrict__ bout,
+                                                                float* __restrict__ emis, int T, int B, int V,
+                                                                float* hlast) {
+    constexpr int H = 32 * NCH;
+    constexpr int AS = H + 8;
+    constexpr int PIECE = 16 * AS;
+    constexpr int NW = NCH;
+    extern __shared__ __attribute__((aligned(16))) __bf16 rxs[];
+    __bf16* hsb = rxs;                                                       // [2][3][16][AS]
+    bf16x8* wof = reinterpret_cast<bf16x8*>(rxs + 2 * 3 * PIECE);            // EMIT: [3][NCH][2][64]
+    float2* ep = reinterpret_cast<float2*>(rxs + 2 * 3 * PIECE + 3 * NCH * 2 * 64 * 8);   // EMIT: [2][NW][4][64]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c15 = lane & 15, gq = lane >> 4;
+    const int r0 = blockIdx.x * 16;
+    bf16x8 bh[2][NCH], bm[2][NCH], bl[2][NCH];
+    int ncol[2];
+    float bias[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        const int n = 32 * w + 16 * ct + c15;
+        ncol[ct] = n;
+        bias[ct] = b_hh[n] + b_ih[n];
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                __bf16 h, m, l;
+                split3(Whh[(long)(32 * c + 8 * gq + j) * H + n], h, m, l);
+                bh[ct][c][j] = h;
+                bm[ct][c][j] = m;
+                bl[ct][c][j] = l;
+            }
+    }
+    // h_{-1} pieces (zeros without h0, RNN.h:15-16) into buffer 0
+    for (int x = tid; x < 16 * H; x += 64 * NW) {
+        const int r = x / H, k = x - r * H;
+        const float v = (h0 && r0 + r < B) ? h0[(long)(r0 + r) * H + k] : 0.f;
+        __bf16 a, b, c;
+        split3(v, a, b, c);
+        hsb[r * AS + k] = a;
+        hsb[PIECE + r * AS + k] = b;
+        hsb[2 * PIECE + r * AS + k] = c;
+    }
+    float bo0 = 0.f, bo1 = 0.f;
+    if (EMIT) {
+        // W_out pieces in MFMA B-fragment order: fragment (piece, chunk, vt),
+        // lane l: W_out[32 chunk + 8 (l >> 4) + j][16 vt + (l & 15)], j < 8
+        for (int x = tid; x < NCH * 2 * 64; x += 64 * NW) {
+            const int l = x & 63, vt = (x >> 6) & 1, c = x >> 7;
+            const int col = 16 * vt + (l & 15);
+            bf16x8 fh, fm, fl;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = 32 * c + 8 * (l >> 4) + j;
+                __bf16 a, b, cc;
+                split3(col < V ? Wout[(long)k * V + col] : 0.f, a, b, cc);
+                fh[j] = a;
+                fm[j] = b;
+                fl[j] = cc;
+            }
+            wof[(0 * NCH + c) * 128 + vt * 64 + l] = fh;
+            wof[(1 * NCH + c) * 128 + vt * 64 + l] = fm;
+            wof[(2 * NCH + c) * 128 + vt * 64 + l] = fl;
+        }
+        for (int x = tid; x < 2 * NW * 4 * 64; x += 64 * NW) ep[x] = float2{0.f, 0.f};
+        bo0 = c15 < V ? bout[c15] : 0.f;
+        bo1 = 16 + c15 < V ? bout[16 + c15] : 0.f;
+    }
+    const long tstride = (long)B * H;
+    const long slab = tstride * 4;
+    int voff[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) voff[ct] = ((r0 + 4 * gq) * H + ncol[ct]) * 4;
+    float pn[2][4];
+    {
+        const auto rs = brsrc(hid, slab);
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) pn[ct][j] = bload(rs, voff[ct] + j * H * 4);
+    }
+    float* const hdst = EMIT ? hout : hid;
+    // EMIT: partial of the h held in hs[buf] over k-chunk w
+    auto emit_partial = [&](const __bf16* pb, f32x4 (&ea)[2]) {
+        ea[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ea[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int off = c15 * AS + 32 * w + 8 * gq;
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(pb + off);
+        const bf16x8 am = *reinterpret_cast<const bf16x8*>(pb + PIECE + off);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
+        // one vocabulary tile at a time (its three W_out fragments live
+        // only for its six MFMAs: the W_hh pieces leave few registers)
+#pragma unroll
+        for (int vt = 0; vt < 2; vt++) {
+            bf16x8 oh[1][1], om[1][1], ol[1][1];
+            oh[0][0] = wof[(0 * NCH + w) * 128 + vt * 64 + lane];
+            om[0][0] = wof[(1 * NCH + w) * 128 + vt * 64 + lane];
+            ol[0][0] = wof[(2 * NCH + w) * 128 + vt * 64 + lane];
+            f32x4 e1[1] = {ea[vt]};
+            X3_PRODUCTS(1, e1, ah, am, al, oh, om, ol, 0)
+            ea[vt] = e1[0];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    auto store_partial = [&](int s, const f32x4 (&ea)[2]) {
+        float2* pp = ep + ((s & 1) * NW + w) * 4 * 64;
+#pragma unroll
+        for (int j = 0; j < 4; j++) pp[j * 64 + lane] = float2{ea[0][j], ea[1][j]};
+    };
+    auto dpp_max16 = [](float x) {
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false)));
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false)));
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false)));
+        x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false)));
+        return x;
+    };
+    auto dpp_sum16 = [](float x) {
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false));
+        return x;
+    };
+    // emissions of frame s from partial buffer s & 1: wave j < 4 owns rows
+    // 4g + j (register j of the C fragments), columns c15 and 16 + c15
+    auto emit_rows = [&](int s, bool store) {
+        const float2* pp = ep + (s & 1) * NW * 4 * 64;
+        for (int j = w; j < 4; j += NW) {
+            float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NW; q++) {
+                const float2 x = pp[(q * 4 + j) * 64 + lane];
+                v0 += x.x;
+                v1 += x.y;
+            }
+            v0 = c15 < V ? v0 + bo0 : -INFINITY;
+            v1 = 16 + c15 < V ? v1 + bo1 : -INFINITY;
+            const float mx = dpp_max16(fmaxf(v0, v1));
+            const float se = dpp_sum16((c15 < V ? expf(v0 - mx) : 0.f) + (16 + c15 < V ? expf(v1 - mx) : 0.f));
+            const float lz = mx + logf(se);
+            const int row = r0 + 4 * gq + j;
+            if (store && row < B) {
+                float* er = emis + ((long)s * B + row) * V;
+                if (c15 < V) er[c15] = v0 - lz;
+                if (16 + c15 < V) er[16 + c15] = v1 - lz;
+            }
+        }
+    };
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < T; t++) {
+        float p[2][4];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) p[ct][j] = pn[ct][j];
+        {
+            const auto rn = brsrc(hid + (t + 1 < T ? t + 1 : t) * tstride, slab);
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) pn[ct][j] = bload(rn, voff[ct] + j * H * 4);
+        }
+        const __bf16* pb = hsb + cur * 3 * PIECE;
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int off = c15 * AS + 32 * c + 8 * gq;
+            const bf16x8 ah = *reinterpret_cast<const bf16x8*>(pb + off);
+            const bf16x8 am = *reinterpret_cast<const bf16x8*>(pb + PIECE + off);
+            const bf16x8 al = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
+            X3_PRODUCTS(2, acc, ah, am, al, bh, bm, bl, c)
+        }
+        __bf16* hn = hsb + (cur ^ 1) * 3 * PIECE;
+        const auto rs = brsrc(hdst + t * tstride, (!EMIT || hdst) ? slab : 0);
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float h = tanhf((p[ct][j] + acc[ct][j]) + bias[ct]);
+                __bf16 a, b, c;
+                split3(h, a, b, c);
+                const int o = (4 * gq + j) * AS + ncol[ct];
+                hn[o] = a;
+                hn[PIECE + o] = b;
+                hn[2 * PIECE + o] = c;
+                bstore(rs, voff[ct] + j * H * 4, h);
+            }
+        }
+        if (EMIT) {
+            // after h_t (acc, P_t dead: fewer live registers): h_{t-1}'s
+            // partial (h_{t-1} is in buffer cur, not overwritten before the
+            // barrier; at t = 0 a dummy into the other partial buffer, never
+            // read) and h_{t-2}'s emissions
+            f32x4 ea[2];
+            emit_partial(pb, ea);
+            emit_rows(t - 2, t >= 2);
+            store_partial(t + 1, ea);
+        }
+        cur ^= 1;
+        lds_barrier_x3();
+    }
+    const __bf16* pl = hsb + cur * 3 * PIECE;   // h_{T-1}
+    if (HL && hlast) {
+        for (int x = tid; x < 16 * H; x += 64 * NW) {
+            const int r = x / H, k = x - r * H;
+            const int o = r * AS + k;
+            if (r0 + r < B) hlast[(long)(r0 + r) * H + k] = ((float)pl[o] + (float)pl[PIECE + o]) + (float)pl[2 * PIECE + o];
+        }
+    }
+    if (EMIT) {   // the last two frames' emissions
+        f32x4 ea[2];
+        emit_partial(pl, ea);
+        if (T >= 2) emit_rows(T - 2, true);
+        store_partial(T - 1, ea);
+        lds_barrier_x3();
+        emit_rows(T - 1, true);
+    }
+}
+
+template <int NCH, bool EMIT, bool HL>
+static int launch_recur_x3_k(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                             float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int V,
+                             float* hlast, hipStream_t s) {
+    constexpr int lds = x3_recur_lds<NCH, EMIT>();
+    static bool attr = false;
+    if (!attr) {
+        ASR_HIP_TRY(hipFuncSetAttribute((const void*)rnn_recur_x3_kernel<NCH, EMIT, HL>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL((rnn_recur_x3_kernel<NCH, EMIT, HL>), dim3((unsigned)((B + 15) / 16)), dim3(64 * NCH), lds,
+                       s, h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+template <bool EMIT, bool HL>
+static int launch_recur_x3(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                           float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int H,
+                           int V, float* hlast, hipStream_t s) {
+    switch (H) {
+        case 64: return launch_recur_x3_k<2, EMIT, HL>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
+        case 128: return launch_recur_x3_k<4, EMIT, HL>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
+        case 256: return launch_recur_x3_k<8, EMIT, HL>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
+        default: return ASR_ERR_UNSUPPORTED;
+    }
+}
+
+bool rnn_x3_applies(int B, int H) {
+    return (H == 64 || H == 128 || H == 256) && B > 0 && (long)B * H * 4 < 0x7fffffffL;
+}
+
+int rnn_recur_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                        int T, int B, int H, hipStream_t s) {
+    if (!rnn_x3_applies(B, H) || T <= 0) return ASR_ERR_UNSUPPORTED;
+    return launch_recur_x3<false, false>(h0, Whh, b_ih, b_hh, hid, nullptr, nullptr, nullptr, nullptr, T, B, H, 0,
+                                         nullptr, s);
+}
+
+int rnn_emit_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, const float* P,
+                       float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int H, int V,
+                       hipStream_t s, float* hlast) {
+    if (!rnn_x3_applies(B, H) || T <= 0 || V < 1 || V > RX_VMAX) return ASR_ERR_UNSUPPORTED;
+    if (hlast)
+        return launch_recur_x3<true, true>(h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B,
+                                           H, V, hlast, s);
+    return launch_recur_x3<true, false>(h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B, H,
+                                        V, nullptr, s);
+}
+
+}  // namespace asr

@@ -344,6 +344,18 @@ static int rnn_frames_eager(const float* h0, const float* W_hh, const float* b_i
     return ASR_OK;
 }
 
+int asr_set_dense_arith(int arith) {
+    if (arith != ASR_DENSE_F32 && arith != ASR_DENSE_SPLIT_BF16) return ASR_ERR_ARG;
+    asr::dense_arith_set(arith);
+    return ASR_OK;
+}
+
+int asr_get_dense_arith(int* arith) {
+    if (!arith) return ASR_ERR_ARG;
+    *arith = asr::dense_arith();
+    return ASR_OK;
+}
+
 int asr_rnn_set_recurrence(int kind) {
     if (kind != ASR_RNN_RECUR_AUTO && kind != ASR_RNN_RECUR_VALU && kind != ASR_RNN_RECUR_MFMA) return ASR_ERR_ARG;
     g_rnn_recur_kind.store(kind, std::memory_order_relaxed);

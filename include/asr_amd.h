@@ -140,6 +140,23 @@ enum { ASR_RNN_RECUR_AUTO = 0, ASR_RNN_RECUR_VALU = 1, ASR_RNN_RECUR_MFMA = 2 };
 int asr_rnn_set_recurrence(int kind);
 int asr_rnn_get_recurrence(int* kind);
 
+/* Arithmetic of the dense fp32 contractions (GEMMs with K <= 256 and N >= 64,
+ * the MFMA recurrence and the fused emission recurrence at H = 64 / 128 / 256),
+ * process-wide:
+ * ASR_DENSE_F32 — v_mfma_f32_16x16x4_f32 (fp32 operands);
+ * ASR_DENSE_SPLIT_BF16 (default; ASR_DENSE=f32 in the environment selects
+ *   the other at start-up) — every fp32 operand split into three bf16 pieces
+ *   (x = h + m + l exactly) and the six significant piece products summed on
+ *   v_mfma_f32_16x16x32_bf16 in fp32: as accurate as the fp32 kernels
+ *   (max error against fp64 / sum |x.y|: 2.2e-7 vs 3.3e-7 for an fp32 FMA
+ *   chain; tests/test_dense_x3_gpu.py), 2.7x their MFMA rate.
+ * Both agree with the reference's fp32 cuBLAS to fp32 rounding, not bit for
+ * bit; the choice depends on this setting and the shape only (never on M),
+ * so an utterance's bits do not depend on its batch. */
+enum { ASR_DENSE_F32 = 0, ASR_DENSE_SPLIT_BF16 = 1 };
+int asr_set_dense_arith(int arith);
+int asr_get_dense_arith(int* arith);
+
 /* The recurrence and the emission layer in one pass — RNN::forward's
  * recurrence (RNN.cu:9-30) followed by Linear::forward (Linear.cu:42-49) with
  * the log_softmax of baseline/model.py:49, for the acoustic model's last RNN

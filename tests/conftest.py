@@ -15,8 +15,10 @@ from pathlib import Path
 # The pipeline's schedules are measured with one hardware queue per stream
 # (bench.py sets the same before the HIP runtime starts); asr_pipeline_create
 # fits its schedule to the queue count it reads (tests/test_pipeline_gpu.py
-# checks the fit at HIP's default of 4 by overriding what it reads).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "24")
+# checks the fit at HIP's default of 4 by overriding what it reads).  Set,
+# not defaulted: a box may export HIP's default of 4.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 try:
     import torch  # noqa: F401  (see module docstring)

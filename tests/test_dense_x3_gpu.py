@@ -1,0 +1,178 @@
+"""GPU numerics of the split-bf16 dense kernels (csrc/dense_x3.hip).
+
+Every fp32 operand is split into three bf16 pieces (x = h + m + l exactly)
+and the six significant piece products are summed on the bf16 matrix cores in
+fp32.  The claim is fp32 accuracy: against an fp64 computation of the same
+sums the split kernels' error must be no larger than the fp32 MFMA kernels'
+(ASR_DENSE_F32) on the same inputs, up to a small margin for two different
+rounding sequences — measured as max |err| / sum_k |a_k b_k| for GEMMs
+(tolerance 1e-6; both measure 1e-7-3e-7), and as max |err| against an fp64
+recurrence for the RNN (tolerance 2e-6 over 40 steps).  The setting and the
+shape alone pick the kernel: a row's bits do not depend on M.
+"""
+import numpy as np
+import pytest
+
+from conftest import asr
+
+pytestmark = pytest.mark.gpu
+
+
+def dm(a):
+    return asr.DeviceMatrix.from_numpy(np.asarray(a, np.float32))
+
+
+@pytest.fixture
+def arith():
+    """Restore the process-wide setting after a test that changes it."""
+    before = asr.get_dense_arith()
+    yield
+    asr.set_dense_arith(before)
+
+
+def test_default_and_roundtrip(arith):
+    assert asr.get_dense_arith() == asr.DENSE_SPLIT_BF16
+    asr.set_dense_arith(asr.DENSE_F32)
+    assert asr.get_dense_arith() == asr.DENSE_F32
+    with pytest.raises(Exception, match="asr_set_dense_arith"):
+        asr.set_dense_arith(7)
+    assert asr.get_dense_arith() == asr.DENSE_F32
+
+
+def _gemm(x, W, b, epi, arith_kind):
+    asr.set_dense_arith(arith_kind)
+    y = asr.DeviceMatrix(x.shape[0], W.shape[1])
+    asr.linear_fwd(dm(x), dm(W), dm(b.reshape(-1, 1)), y, epi)
+    return y.toCpu()
+
+
+@pytest.mark.parametrize("M,K,N,epi", [(1000, 256, 256, "bias"), (333, 96, 200, "none"), (64, 32, 64, "relu"),
+                                       (4099, 128, 512, "bias"), (2000, 200, 300, "none"), (17, 4, 70, "bias"),
+                                       (140000, 256, 256, "none")])
+def test_gemm_fp32_accuracy(M, K, N, epi, arith):
+    """Split-bf16 GEMM vs fp64: error / sum|a b| <= 1e-6 and no worse than the
+    fp32 MFMA kernel's (x 1.5 + 1e-8); ragged M, K not a multiple of 32, N
+    not a multiple of 256 (column masks), several column blocks."""
+    rng = np.random.default_rng(M + K + N)
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = (rng.uniform(-1, 1, (K, N)) / np.sqrt(K)).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, N).astype(np.float32)
+    code = {"none": asr.EPI_NONE, "bias": asr.EPI_BIAS, "relu": asr.EPI_BIAS_RELU}[epi]
+    rows = np.unique(np.concatenate([np.arange(min(M, 256)), rng.integers(0, M, 256), [M - 1]]))
+    xs, Wd = x[rows].astype(np.float64), W.astype(np.float64)
+    ref = xs @ Wd
+    scale = np.abs(xs) @ np.abs(Wd)
+    if epi != "none":
+        ref = ref + b
+        scale = scale + np.abs(b)
+    if epi == "relu":
+        ref = np.maximum(ref, 0)
+    errs = {}
+    for kind in (asr.DENSE_SPLIT_BF16, asr.DENSE_F32):
+        got = _gemm(x, W, b, code, kind)[rows].astype(np.float64)
+        errs[kind] = float((np.abs(got - ref) / scale).max())
+    assert errs[asr.DENSE_SPLIT_BF16] <= 1e-6, errs
+    assert errs[asr.DENSE_SPLIT_BF16] <= 1.5 * errs[asr.DENSE_F32] + 1e-8, errs
+
+
+def test_gemm_rows_independent_of_m(arith):
+    """The rows of a sub-batch are the same bits as in the whole batch (the
+    kernel choice depends on the shape's K / N only), and the transposed-B
+    form agrees with the row-major one."""
+    asr.set_dense_arith(asr.DENSE_SPLIT_BF16)
+    rng = np.random.default_rng(3)
+    M, K, N = 5000, 256, 256
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = (rng.uniform(-1, 1, (K, N)) / 16).astype(np.float32)
+    full = asr.DeviceMatrix(M, N)
+    asr.linear_fwd(dm(x), dm(W), None, full, asr.EPI_NONE)
+    full = full.toCpu()
+    for lo, hi in ((0, 16), (7, 1000), (4096, 5000)):
+        part = asr.DeviceMatrix(hi - lo, N)
+        asr.linear_fwd(dm(x[lo:hi]), dm(W), None, part, asr.EPI_NONE)
+        assert np.array_equal(part.toCpu(), full[lo:hi]), (lo, hi)
+    # z = x . (W^T)^T through asr_matmul_tb: B read with strides, same products
+    z = asr.DeviceMatrix(M, N)
+    import ctypes
+    Wt = dm(np.ascontiguousarray(W.T))
+    xd = dm(x)
+    asr.check(asr.lib().asr_matmul_tb(xd.ptr, Wt.ptr, z.ptr, M, K, N, None), "asr_matmul_tb")
+    assert np.array_equal(z.toCpu(), full)
+
+
+def _rnn64(P, T, B, w_hh, b, h0=None):
+    H = w_hh.shape[0]
+    h = np.zeros((B, H)) if h0 is None else h0.astype(np.float64)
+    out = np.empty((T, B, H))
+    W = w_hh.astype(np.float64)
+    for t in range(T):
+        h = np.tanh(P[t].astype(np.float64) + h @ W + b)
+        out[t] = h
+    return out
+
+
+@pytest.mark.parametrize("T,B,H", [(40, 37, 256), (40, 64, 128), (25, 16, 64), (3, 5, 256)])
+def test_recurrence_fp32_accuracy(T, B, H, arith, monkeypatch):
+    """The split-bf16 MFMA recurrence (ASR_RNN_MFMA=1) vs an fp64 recurrence:
+    max |err| <= 2e-6 and no worse than the fp32 MFMA kernel's (x 1.5 +
+    2e-7), with and without h0, ragged last utterance tile."""
+    monkeypatch.setenv("ASR_RNN_MFMA", "1")
+    rng = np.random.default_rng(T + B + H)
+    s = 1 / np.sqrt(H)
+    P = rng.uniform(-1, 1, (T, B, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32)
+    bias = b_hh.astype(np.float64) + b_ih.astype(np.float64)
+    for h0n in (None, h0):
+        ref = _rnn64(P, T, B, w_hh, bias, h0n)
+        errs = {}
+        for kind in (asr.DENSE_SPLIT_BF16, asr.DENSE_F32):
+            asr.set_dense_arith(kind)
+            hid = dm(P.reshape(T * B, H))
+            asr.rnn_recur_fwd(dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), hid, T, B,
+                              h0=None if h0n is None else dm(h0n))
+            errs[kind] = float(np.abs(hid.toCpu().reshape(T, B, H) - ref).max())
+        assert errs[asr.DENSE_SPLIT_BF16] <= 2e-6, errs
+        assert errs[asr.DENSE_SPLIT_BF16] <= 1.5 * errs[asr.DENSE_F32] + 2e-7, errs
+
+
+@pytest.mark.parametrize("T,B,H,V", [(30, 37, 256, 29), (1, 5, 256, 29), (2, 16, 128, 32), (12, 33, 64, 7),
+                                     (20, 256, 256, 29)])
+def test_emit_fp32_accuracy(T, B, H, V, arith):
+    """asr_rnn_emit_fwd on the split arithmetic vs fp64 (recurrence, h.W_out +
+    b_out, log_softmax): emissions within 5e-6 and no worse than the fp32
+    kernel's (x 1.5 + 5e-7); its hidden states are the split recurrence's
+    bits; a segmented run (h_{T-1} carried, asr_pipeline's segments) is not
+    exposed here — tests/test_pipeline_gpu.py checks it bit for bit."""
+    rng = np.random.default_rng(T * 3 + B + H + V)
+    s = 1 / np.sqrt(H)
+    P = rng.uniform(-1, 1, (T, B, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    w_out = rng.uniform(-4 * s, 4 * s, (H, V)).astype(np.float32)
+    b_out = rng.uniform(-0.5, 0.5, V).astype(np.float32)
+    h64 = _rnn64(P, T, B, w_hh, b_hh.astype(np.float64) + b_ih.astype(np.float64))
+    z = h64 @ w_out.astype(np.float64) + b_out
+    z = z - z.max(axis=-1, keepdims=True)
+    eref = z - np.log(np.exp(z).sum(axis=-1, keepdims=True))
+    W = [dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), dm(w_out), dm(b_out.reshape(V, 1))]
+    errs, hids = {}, {}
+    for kind in (asr.DENSE_SPLIT_BF16, asr.DENSE_F32):
+        asr.set_dense_arith(kind)
+        em, hid = asr.DeviceMatrix(T * B, V), asr.DeviceMatrix(T * B, H)
+        asr.rnn_emit_fwd(*W, dm(P.reshape(T * B, H)), em, T, B, hid=hid)
+        errs[kind] = float(np.abs(em.toCpu().reshape(T, B, V) - eref).max())
+        hids[kind] = hid.toCpu()
+    assert errs[asr.DENSE_SPLIT_BF16] <= 5e-6, errs
+    assert errs[asr.DENSE_SPLIT_BF16] <= 1.5 * errs[asr.DENSE_F32] + 5e-7, errs
+    asr.set_dense_arith(asr.DENSE_SPLIT_BF16)
+    hid2 = dm(P.reshape(T * B, H))
+    asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
+    try:
+        asr.rnn_recur_fwd(W[0], W[1], W[2], hid2, T, B)
+    finally:
+        asr.rnn_set_recurrence(asr.RNN_RECUR_AUTO)
+    assert np.array_equal(hid2.toCpu(), hids[asr.DENSE_SPLIT_BF16])
