@@ -41,6 +41,7 @@ checked bit for bit against a 1-GPU decode of the same utterance ids on rank
                     [--global-batch G | --batch B] [--decode-only] [--no-pipeline]
 """
 import argparse
+import collections
 import ctypes
 import gc
 import hashlib
@@ -361,6 +362,9 @@ def main():
     ap.add_argument("--decode-partition", type=int, default=0,
                     help="batches that fill the chip: decode streams on CUs [0, N), production on the rest "
                          "(0: every stream on every CU)")
+    ap.add_argument("--pipeline-batch", type=int, default=0,
+                    help="utterances per pipeline batch (the rank's B go through as B / N batches; "
+                         "0 = auto: 1024 when B is a larger multiple of it on the split-bf16 arithmetic)")
     ap.add_argument("--py-pipeline", action="store_true",
                     help="the round-2 Python orchestration over torch streams instead of the library's "
                          "native pipeline (asr_pipeline_*); implied by its Python-only knobs")
@@ -773,7 +777,7 @@ def main():
 
 
 def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms, best,
-           dec_config, weights, d_hid0, d_emis0, d_emis_last, sched):
+           dec_config, weights, d_hid0, d_emis0, d_emis_last, sched, parity_src=None):
     """Everything after the timed region: host gather of the hypotheses,
     roofline, GEMM MFMA utilisation, CPU baseline and the JSON line (rank 0)."""
     d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout = weights
@@ -813,8 +817,11 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
     avg_kernel_ms = float(np.mean(kernel_ms)) if kernel_ms else None
     bpf = algorithmic_bytes_per_frame(V, beam)
     roof = None
+    # one decode launch covers a pipeline batch (Bl utterances); the parity
+    # witness is the last collected batch
+    Bl, best_p = parity_src if parity_src else (B, best)
     if avg_kernel_ms:
-        achieved = bpf * B * T / (avg_kernel_ms * 1e-3) / 1e9
+        achieved = bpf * Bl * T / (avg_kernel_ms * 1e-3) / 1e9
         ms_, waves_run, _ = dec_config
         variant = decoder_variant(V, waves_run, ms_)
         wl = args.config + (" decode-only" if args.decode_only else "")
@@ -829,7 +836,7 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "frac_of": "HBM roofline (SURVEY §8(d) algorithmic bytes: 4V + 40K per frame)",
                 "avg_launch_ms": round(avg_kernel_ms, 4), "bytes_per_frame": bpf,
-                "frames_per_launch": B * T, "us_per_frame_step": round(1e3 * avg_kernel_ms / T, 4),
+                "frames_per_launch": Bl * T, "us_per_frame_step": round(1e3 * avg_kernel_ms / T, 4),
                 "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
                 "traffic_source": traffic, "issue": issue,
                 "limiter": "on-chip dependency latency per frame (beam resident in LDS): "
@@ -865,8 +872,8 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
             emis_host, note = d_emis_last
         else:
             emis_host, note = d_emis_last.toCpu(), "the decoded buffer of the timed region's last batch"
-        cpu = cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, B, In, H, V, beam, emis_host,
-                           best, full_T=args.cpu_full_T, emis_note=note)
+        cpu = cpu_baseline(asr, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout, T, Bl, In, H, V, beam, emis_host,
+                           best_p, full_T=args.cpu_full_T, emis_note=note)
         parity = cpu.pop("parity")
 
     if rank == 0:
@@ -906,7 +913,26 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     reading each batch's results once `inflight` newer ones are queued."""
     d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout = weights
     dcus = -1 if args.no_partition else args.decode_partition
-    pl = asr.Pipeline(T, B, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
+    # The rank's B utterances go through the pipeline as B / Bp batches of Bp
+    # (--pipeline-batch; auto: 1024 when B is a multiple of 1024 above it on
+    # the split-bf16 arithmetic — measured at 2048 per GPU: 269 M frames/s as
+    # two 1024-utterance batches against 240 M as one, the two decodes and
+    # two productions in flight overlapping where one 2048 batch serialises
+    # them; profiles/r04/bench_scan.md).  Every step still produces and
+    # decodes all B utterances x T frames.
+    split = asr.get_dense_arith() == asr.DENSE_SPLIT_BF16
+    Bp = args.pipeline_batch or (1024 if split and B > 1024 and B % 1024 == 0 else B)
+    if B % Bp:
+        raise SystemExit(f"--pipeline-batch {Bp} does not divide the {B} utterances per GPU")
+    nsub = B // Bp
+    if nsub > 1:
+        xh = d_x.toCpu().reshape(T, B, In)
+        xs = [asr.DeviceMatrix.from_numpy(np.ascontiguousarray(xh[:, k * Bp:(k + 1) * Bp, :]).reshape(T * Bp, In))
+              for k in range(nsub)]
+        del xh
+    else:
+        xs = [d_x]
+    pl = asr.Pipeline(T, Bp, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
                       inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus)
     desc = pl.describe()
     if desc["mode"] == asr.PIPELINE_MODES[1] and H <= 256:
@@ -921,24 +947,32 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
 
     hostlog = [] if os.environ.get("ASR_BENCH_HOSTLOG") else None   # diagnostic: host call times
 
+    # one result slot per sub-batch (collects come in submission order, so
+    # the last step's B utterances end up in slots 0 .. nsub-1, in order)
+    _l, _n, _p = pl._lab, pl._len, pl._lp
+    slots = [(np.empty_like(_l), np.empty_like(_n), np.empty_like(_p)) for _ in range(nsub)]
+
     def take():
-        lab, ln, lp, ms = pl.collect()
+        lab, ln, lp, ms = pl.collect(out=slots[take.j % nsub])
+        take.j += 1
         kernel_ms.append(ms)
-        best["arrays"] = (lab, ln, lp)
         if hostlog is not None:
             hostlog.append(("collect", time.perf_counter()))
 
     def run(n):
-        for _ in range(n):
-            pl.submit(d_x)
+        for _ in range(n * nsub):
+            pl.submit(xs[run.k % nsub])
+            run.k += 1
             if hostlog is not None:
                 hostlog.append(("submit", time.perf_counter()))
             while pl.pending() > lag:
                 take()
         while pl.pending():
             take()
+    run.k = 0
+    take.j = 0
 
-    run(2 * (desc["inflight"] + desc["prod_streams"]) + 1)   # every buffer, stream and workspace once
+    run(-(-(2 * (desc["inflight"] + desc["prod_streams"]) + 1) // nsub))   # every buffer, stream and workspace once
     run(args.warmup)
     kernel_ms.clear()
     if world > 1:
@@ -959,7 +993,12 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     if world > 1:
         dist.barrier()
     desc = pl.describe()
-    lab, ln, lp = (a.copy() for a in best["arrays"])
+    assert take.j % nsub == 0 and run.k % nsub == 0
+    last = [tuple(a.copy() for a in r) for r in slots]
+    lab_p, ln_p, lp_p = last[-1]   # the last collected batch: the parity witness's
+    lab = np.concatenate([r[0] for r in last])
+    ln = np.concatenate([r[1] for r in last])
+    lp = np.concatenate([r[2] for r in last])
     Kb = beam + 1
     kcap = -(-(Kb + max(8, Kb // 8)) // 32) * 32
     # buffers for the GEMM timing
@@ -971,9 +1010,10 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
         # parity witness of the measured path), and a check that
         # model_emissions reproduces them (the 1-GPU re-decode relies on it)
         em_last = pl.peek_emissions()
-        asr.model_emissions(d_x, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, B, em0, fused, work=hid0,
+        em_chk, wk = (em0, hid0) if nsub == 1 else (asr.DeviceMatrix(T * Bp, V), asr.DeviceMatrix(T * Bp, H))
+        asr.model_emissions(xs[-1], [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout], T, Bp, em_chk, fused, work=wk,
                             recurrence=desc["recurrence"])
-        same = bool(np.array_equal(em0.toCpu().reshape(T, B, V), em_last))
+        same = bool(np.array_equal(em_chk.toCpu().reshape(T, Bp, V), em_last))
         em_last = (em_last, "the pipeline's own emission buffer of the timed region's last batch "
                             "(asr_pipeline_peek_emissions); model_emissions reproduces it bit for bit: "
                             + ("yes" if same else "NO"))
@@ -981,13 +1021,15 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             raise SystemExit("model_emissions does not reproduce the pipeline's emissions")
     finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
            (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_last,
-           {"inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
+           {"pipeline_batch": Bp, "batches_per_step": nsub,
+            "inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
             "decode_cus": desc["decode_cus"], "fused_emission": fused,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
-                        f"library-owned streams, buffers and decoder schedule"})
+                        f"library-owned streams, buffers and decoder schedule"},
+           parity_src=(Bp, (lab_p, ln_p, lp_p)))
     pl.close()
     asr.synchronize()
 

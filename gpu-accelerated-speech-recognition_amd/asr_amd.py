@@ -641,18 +641,22 @@ class Pipeline:
         check(lib().asr_pipeline_pending(self.h, ctypes.byref(n)), "asr_pipeline_pending")
         return n.value
 
-    def collect(self):
+    def collect(self, out=None):
         """(labels [B][T] int32, lengths [B], logp [B] fp64, decode_ms) of the
-        oldest batch; the arrays are reused by the next call."""
+        oldest batch; the arrays are reused by the next call unless the caller
+        passes its own (out = (labels, lengths, logp) of those shapes / dtypes)."""
         ms = _f()
-        rc = lib().asr_pipeline_collect(self.h, _ptr(self._lab), self._lab.shape[1], _ptr(self._len),
-                                        _ptr(self._lp), ctypes.byref(ms))
+        lab, ln, lp = (self._lab, self._len, self._lp) if out is None else out
+        assert lab.dtype == np.int32 and lab.shape == self._lab.shape and lab.flags.c_contiguous
+        assert ln.dtype == self._len.dtype and ln.shape == self._len.shape
+        assert lp.dtype == np.float64 and lp.shape == self._lp.shape
+        rc = lib().asr_pipeline_collect(self.h, _ptr(lab), lab.shape[1], _ptr(ln), _ptr(lp), ctypes.byref(ms))
         n = _i()
         if lib().asr_pipeline_pending(self.h, ctypes.byref(n)) == ASR_OK:
             while len(self._inputs) > n.value:   # collected batches' features may go
                 self._inputs.popleft()
         check(rc, "asr_pipeline_collect")
-        return self._lab, self._len, self._lp, ms.value
+        return lab, ln, lp, ms.value
 
     def peek_emissions(self) -> np.ndarray:
         """Host copy of the emissions [T][B][V] the last collected batch's

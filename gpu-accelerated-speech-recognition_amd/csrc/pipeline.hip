@@ -474,7 +474,12 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // (C3, B = 256, 20 steps: 96 / 112 / 128 / 144 / 160 / 176 / 192
         // decode CUs 59.5 / 72.5 / 88.3 / 79.4 / 77.1 / 57.2 / 61.1 M frames/s,
         // profiles/r04/bench_scan.md).
-        const int dauto = (kcap > 64 ? ncu / 2 : (c.B < 512 ? ncu * 3 / 8 : ncu / 2)) / 8 * 8;
+        // On the split-bf16 arithmetic (dense_x3.hip) production costs ~half
+        // the CU time, and half of the CUs decode at every batch size (256
+        // per GPU, GSPLIT 0: 96 / 112 / 128 decode CUs 162 / 188 / 186 M
+        // frames/s; profiles/r04/bench_scan.md).
+        const bool x3 = asr::dense_x3_on();
+        const int dauto = (kcap > 64 || x3 ? ncu / 2 : (c.B < 512 ? ncu * 3 / 8 : ncu / 2)) / 8 * 8;
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : dauto) : 0;
         const int dc = p->dcus ? p->dcus : ncu;
         // as many batches decoding at once as fill the decode CUs at the
@@ -500,8 +505,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             // CUs (1024 per GPU: 171 vs 180 M at 0.3 / 0), with the tiled one
             // 0 / 0.2 / 0.3 -> 173 / 196 / 198 M, 512 per GPU 167 / 182 / 182 M
             // (profiles/r03/bench_scan.md)
-            // two rows per lane: the decode CUs are the busier half, no share (A/B)
-            const double f = ge ? atof(ge) : (kcap > 64 ? 0.0 : 0.3);
+            // two rows per lane: the decode CUs are the busier half, no share (A/B).
+            // Split-bf16 arithmetic: none either — its GEMM workgroups take a
+            // whole CU (2 waves per SIMD at ~240 VGPRs), so a share on the
+            // decode CUs holds decodes back (256 / 512 / 1024 per GPU at 0.3 vs
+            // 0: 103 / 181 / 205 vs 162 / 242 / 269 M frames/s; 2048: 233 vs
+            // 236 M, 240 M at 0.1)
+            const double f = ge ? atof(ge) : (kcap > 64 || x3 ? 0.0 : 0.3);
             p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
             const char* gt = getenv("ASR_PIPELINE_GTILED");   // A/B: 1 / 0 force, default: D > 1
             p->gtiled = gt ? atoi(gt) != 0 : p->D > 1;

@@ -231,24 +231,26 @@ def test_baseline_harness_workload_e2e():
     d.close()
 
 
-def test_c4_pipeline_full_size_vs_oracle():
+@pytest.mark.parametrize("B", [2048, 1024])
+def test_c4_pipeline_full_size_vs_oracle(B):
     """The bench's headline path exactly: the native
-    pipeline at C4's one-GPU shape (T = 1000, B = 2048, H = 256, V = 29,
-    beam 50) with its automatic schedule — fused recurrence + emission
-    kernel, 30 % of the input-projection rows on the decode CUs, the one-wave
+    pipeline at C4's one-GPU shape (T = 1000, H = 256, V = 29, beam 50; B =
+    2048 as one batch, and 1024: the pipeline batch bench.py feeds C4's 2048
+    utterances per GPU in on the split-bf16 arithmetic) with its automatic
+    schedule — split-bf16 fused recurrence + emission kernel, the one-wave
     decoder 16 to a decode CU — against the oracle on 8 full-length
     utterances spread over the batch, decoded from the very emission bytes
     the pipeline's decode consumed (asr_pipeline_peek_emissions).  The whole
     batch must also equal a sequential decode of model_emissions (the same
     production, one call at a time)."""
-    T, B, H, V, beam = 1000, 2048, 256, 29, 50
+    T, H, V, beam = 1000, 256, 29, 50
     (w_ih, w_hh, b_ih, b_hh), (w_out, b_out) = bench.make_weights(H, H, V)
     DM = asr.DeviceMatrix.from_numpy
     W = [DM(w_ih), DM(w_hh), DM(b_ih.reshape(H, 1)), DM(b_hh.reshape(H, 1)), DM(w_out), DM(b_out.reshape(V, 1))]
     x = DM(bench.make_features(T, B, H, 0))
     p = asr.Pipeline(T, B, H, H, V, beam, W)
     d = p.describe()
-    assert d["mode"] == "chip-filling batches" and d["fused_emission"] and d["decode_cu_gemm_rows"] > 0, d
+    assert d["mode"] == "chip-filling batches" and d["fused_emission"], d
     for _ in range(3):   # three batches in flight through the ring
         p.submit(x)
     outs = []
@@ -265,7 +267,7 @@ def test_c4_pipeline_full_size_vs_oracle():
     em = asr.DeviceMatrix(T * B, V)
     asr.model_emissions(x, W, T, B, em, True)
     assert np.array_equal(em.toCpu().reshape(T, B, V), e), "model_emissions differs from the pipeline's emissions"
-    sub = [0, 293, 585, 878, 1170, 1463, 1755, 2047]
+    sub = sorted({int(round(v)) for v in np.linspace(0, B - 1, 8)})
     ref = oracle.decode(np.ascontiguousarray(e[:, sub, :]), beam, 0, is_log=True, nthreads=cpu_threads(),
                         max_hyps=1)
     for i, u in enumerate(sub):

@@ -246,7 +246,9 @@ def test_pipeline_fits_hw_queues(monkeypatch):
     (streams sharing a hardware queue serialise): at HIP's default of 4 the
     chip-filling schedule drops production streams, then the decode CUs'
     share of the input projection; explicit counts are kept.  The results
-    are the same bits either way."""
+    are the same bits either way.  (The decode CUs' share is requested
+    explicitly: the split-bf16 arithmetic's default is none.)"""
+    monkeypatch.setenv("ASR_PIPELINE_GSPLIT", "0.3")
     T, B, inp, H, V, beam = 24, 600, 64, 256, 29, 30
     W = _weights(inp, H, V, seed=13)
     x = asr.DeviceMatrix.from_numpy(np.random.default_rng(2).uniform(-1, 1, (T * B, inp)).astype(np.float32))
