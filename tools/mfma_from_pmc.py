@@ -3,15 +3,18 @@ passes `mfma` and `valu`) into profiles/<round>/mfma.json and the decoder's
 VALU mix into profiles/<round>/issue.json [workload][variant]["valu_mix"].
 
 mfma pass counters: SQ_VALU_MFMA_BUSY_CYCLES (cycles, 32 per
-v_mfma_f32_16x16x4_f32 per SIMD), SQ_INSTS_VALU_MFMA_F32,
-SQ_INSTS_VALU_MFMA_MOPS_F32, SQ_BUSY_CYCLES, SQ_WAVES, SQ_ACTIVE_INST_ANY,
+v_mfma_f32_16x16x4_f32 and 16 per v_mfma_f32_16x16x32_bf16 per SIMD),
+SQ_INSTS_VALU_MFMA_{F32,BF16}, SQ_INSTS_VALU_MFMA_MOPS_{F32,BF16} (one MOP =
+512 flop), SQ_BUSY_CYCLES, SQ_WAVES, SQ_ACTIVE_INST_ANY,
 GRBM_GUI_ACTIVE (summed over the 8 XCDs: / 8 = the dispatch's wall clock
 cycles), GRBM_COUNT.  Counter passes serialise dispatches, so each one ran
 alone on its stream's CUs.  Per kernel (dispatches grouped by MFMA count, so
 the bench's full-size standalone GEMM and its pipeline slices are apart):
   wall_cycles   = GRBM_GUI_ACTIVE / 8
   mfma_busy     = MFMA_BUSY_CYCLES / (4 SIMDs x cus x wall_cycles)
-  flop          = 512 x MFMA_MOPS_F32 (one MOP = 512 flop)
+  flop          = 512 x MFMA_MOPS_F32 (one MOP = 512 flop); for the split-bf16
+                  kernels (bf16 MFMAs, 6 products per fp32 product) gflop is the
+                  fp32-equivalent 512 x MOPS_BF16 / 6, bf16_gflop the matrix-core work
   clock_ghz     = wall_cycles / dispatch duration
 valu pass counters (decoder): SQ_ACTIVE_INST_VALU, SQ_INSTS_VALU,
 SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, SQ_ACTIVE_INST_SCA, SQ_WAVE_CYCLES.
@@ -50,6 +53,8 @@ def main():
     ap.add_argument("--slice-cus", type=int, default=0,
                     help="CUs of a kernel's smaller dispatch groups (the pipeline's CU-masked slices of a "
                          "GEMM whose full-size standalone run has the most MFMAs)")
+    ap.add_argument("--slice", action="append", default=[],
+                    help="kernel=CUs of that kernel's smaller dispatch groups (overrides --slice-cus)")
     ap.add_argument("--T", type=int, required=True)
     ap.add_argument("--B", type=int, required=True)
     ap.add_argument("--decoder", default="ctc_wave_kernel")
@@ -62,22 +67,27 @@ def main():
     groups = collections.defaultdict(list)
     for d, c in per.items():
         name, secs = meta[d]
-        if c.get("SQ_INSTS_VALU_MFMA_F32", 0) <= 0:
+        n = c.get("SQ_INSTS_VALU_MFMA_F32", 0) + c.get("SQ_INSTS_VALU_MFMA_BF16", 0)
+        if n <= 0:
             continue
-        groups[(name, round(c["SQ_INSTS_VALU_MFMA_F32"]))].append((c, secs))
+        groups[(name, round(n))].append((c, secs))
     out = {}
     biggest = {}
     for (name, nmfma) in groups:
         biggest[name] = max(biggest.get(name, 0), nmfma)
     for (name, nmfma), lst in sorted(groups.items()):
         ncu = next((int(v) for k, v in cus.items() if k in name), 256)
-        if args.slice_cus and nmfma < biggest[name]:
-            ncu = args.slice_cus
+        if nmfma < biggest[name]:
+            sl = next((int(v) for k, v in (x.split("=") for x in args.slice) if k in name), args.slice_cus)
+            ncu = sl or ncu
         avg = {k: sum(c[k] for c, _ in lst) / len(lst) for k in lst[0][0]}
         secs = sum(s for _, s in lst) / len(lst)
         wall = avg["GRBM_GUI_ACTIVE"] / 8.0
+        bf16 = 512.0 * avg.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) / 1e9
         rec = {"dispatches": len(lst), "cus": ncu, "mfma_f32_insts": round(avg["SQ_INSTS_VALU_MFMA_F32"]),
-               "gflop": round(512.0 * avg["SQ_INSTS_VALU_MFMA_MOPS_F32"] / 1e9, 2),
+               "mfma_bf16_insts": round(avg.get("SQ_INSTS_VALU_MFMA_BF16", 0.0)),
+               "gflop": round(512.0 * avg["SQ_INSTS_VALU_MFMA_MOPS_F32"] / 1e9 + bf16 / 6.0, 2),
+               "bf16_gflop": round(bf16, 2),
                "mfma_busy_cycles": round(avg["SQ_VALU_MFMA_BUSY_CYCLES"]),
                "wall_cycles": round(wall), "duration_ms": round(1e3 * secs, 4),
                "clock_ghz": round(wall / secs / 1e9, 3) if secs > 0 else None,

@@ -21,7 +21,8 @@ SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY
 # the decoder's VALU mix (fp64 share, VALU issue cycles) and the scalar unit
 VALU="SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES"
 # matrix-core evidence of the dense kernels (+ the clock)
-MFMA="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
+# (fp32 MFMAs: the fp32 kernels and the emission GEMM; bf16 MFMAs: the split-bf16 kernels, dense_x3.hip)
+MFMA="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_BF16 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
 for pass in ${PASSES:-trace fetch write}; do
     case $pass in
         trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
