@@ -245,6 +245,26 @@ def load_counters(name: str, workload: str, variant: str):
     return None
 
 
+def load_kernel_stats(workload: str, variant: str):
+    """rocprofv3 --kernel-trace --stats average dispatch duration of this
+    kernel variant in the committed trace of this bench workload
+    (profiles/<round>/<workload>_final_kernel_stats.csv), or None."""
+    import csv as _csv
+    for rnd in PROFILE_ROUNDS:
+        p = ROOT / "profiles" / rnd / f"{workload.lower()}_final_kernel_stats.csv"
+        if not p.exists():
+            continue
+        try:
+            for r in _csv.DictReader(open(p)):
+                name = r["Name"].split("(")[0].replace("void ", "").replace("asr::", "").replace(" ", "")
+                if name == variant:
+                    return {"avg_ms": round(float(r["AverageNs"]) * 1e-6, 4), "calls": int(r["Calls"]),
+                            "source": f"profiles/{rnd}/{p.name}"}
+        except Exception:
+            continue
+    return None
+
+
 def load_mfma_counters(workload: str):
     """Counter evidence of the dense kernels (profiles/<round>/mfma.json, from
     tools/mfma_from_pmc.py over a rocprofv3 --pmc pass of this bench):
@@ -839,6 +859,11 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                 "frames_per_launch": Bl * T, "us_per_frame_step": round(1e3 * avg_kernel_ms / T, 4),
                 "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
                 "traffic_source": traffic, "issue": issue,
+                # avg_launch_ms is the HIP-event span on the decode stream: with
+                # one decode queued beyond those the decode CUs hold it includes
+                # that decode's wait for CUs; rocprofv3's dispatch duration of
+                # the same kernel in the committed trace of this workload:
+                "rocprof_kernel": load_kernel_stats(wl, variant),
                 "limiter": "on-chip dependency latency per frame (beam resident in LDS): "
                            "see roofline.issue for the measured issue/wait fractions"}
 
