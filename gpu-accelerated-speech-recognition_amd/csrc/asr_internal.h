@@ -40,6 +40,11 @@ extern thread_local int asr_internal_gemm_tiled;
 // recurrence launches (H > 256) into the library's HIP graph at their first
 // use, not the second (a pipeline's buffers recur; one-off calls stay eager).
 extern thread_local int asr_internal_graph_now;
+// Dense arithmetic for this thread's next dense calls (ASR_DENSE_*; -1: the
+// process-wide asr_set_dense_arith setting).  A pipeline latches the setting
+// it was created under and sets this around its own calls, so a later change
+// of the process-wide setting never changes a running pipeline's bits.
+extern thread_local int asr_internal_dense_arith;
 // One-wave decoder workgroups (utterances) that fit on one CU for this
 // handle's layout (the occupancy query); 0 when the one-wave kernel does not
 // apply (V > 63, .cu semantics, timesteps).  For the pipeline's schedule.

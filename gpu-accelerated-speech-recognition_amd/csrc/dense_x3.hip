@@ -25,12 +25,15 @@
 #include <cstdlib>
 #include <cstring>
 
+thread_local int asr_internal_dense_arith = -1;
+
 namespace asr {
 
 // ASR_DENSE_F32 / ASR_DENSE_SPLIT_BF16 (asr_set_dense_arith); initial value
 // from ASR_DENSE ("f32" / "x3"), else the split arithmetic.
 static std::atomic<int> g_dense_arith{-1};
 int dense_arith() {
+    if (asr_internal_dense_arith >= 0) return asr_internal_dense_arith;   // a pipeline's latched setting
     int a = g_dense_arith.load(std::memory_order_relaxed);
     if (a < 0) {
         const char* e = getenv("ASR_DENSE");

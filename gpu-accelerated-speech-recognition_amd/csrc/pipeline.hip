@@ -66,6 +66,7 @@ struct asr_pipeline {
     const float *W_ih = nullptr, *W_hh = nullptr, *b_ih = nullptr, *b_hh = nullptr;
     const float *W_out = nullptr, *b_out = nullptr;
     int ncu = 0, mode = SHARED, D = 1, P = 1, nbuf = 2, gcu = 0, dcus = 0, rnn_kind = -1;
+    int arith = -1;       // the dense arithmetic latched at creation (asr_internal_dense_arith)
     bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
     bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
@@ -132,6 +133,14 @@ int cu_stream(hipStream_t* s, int ncu, int lo, int hi) {
     ASR_HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)words, m.data()));
     return ASR_OK;
 }
+
+// Sets this thread's dense arithmetic to a pipeline's latched one for the
+// scope of a pipeline call (restores the previous value).
+struct ArithGuard {
+    int prev;
+    explicit ArithGuard(int a) : prev(asr_internal_dense_arith) { asr_internal_dense_arith = a; }
+    ~ArithGuard() { asr_internal_dense_arith = prev; }
+};
 
 // Production of batch i into buffer k (unsplit): RNN forward + emission projection.
 int produce_full(asr_pipeline* p, long i, const float* x) {
@@ -432,6 +441,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         }
     }
     p->W_ih = W_ih; p->W_hh = W_hh; p->b_ih = b_ih; p->b_hh = b_hh; p->W_out = W_out; p->b_out = b_out;
+    p->arith = asr::dense_arith();
+    ArithGuard arith_guard(p->arith);
     int dev = 0;
     int rc = ASR_OK;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -646,6 +657,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
 
 int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
     if (!p || !x) return ASR_ERR_ARG;
+    ArithGuard arith_guard(p->arith);
     if (p->fail_rc) return p->fail_rc;
     const long i = p->submitted;
     // buffer i % nbuf is reused: its previous batch's results must be fetched first
@@ -703,6 +715,7 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
 int asr_pipeline_collect(asr_pipeline_t* p, int32_t* labels, int max_len, int32_t* lengths, double* logp,
                          float* decode_ms) {
     if (!p || (!labels && max_len > 0)) return ASR_ERR_ARG;
+    ArithGuard arith_guard(p->arith);   // a drain may queue held-back production
     if (p->stash.empty()) {   // the common case: straight into the caller's arrays
         long batch = -1;
         int res = ASR_OK;

@@ -152,7 +152,8 @@ int asr_rnn_get_recurrence(int* kind);
  *   chain; tests/test_dense_x3_gpu.py), 2.7x their MFMA rate.
  * Both agree with the reference's fp32 cuBLAS to fp32 rounding, not bit for
  * bit; the choice depends on this setting and the shape only (never on M),
- * so an utterance's bits do not depend on its batch. */
+ * so an utterance's bits do not depend on its batch.  A pipeline keeps the
+ * setting it was created under for all its batches. */
 enum { ASR_DENSE_F32 = 0, ASR_DENSE_SPLIT_BF16 = 1 };
 int asr_set_dense_arith(int arith);
 int asr_get_dense_arith(int* arith);

@@ -273,3 +273,38 @@ def test_pipeline_fits_hw_queues(monkeypatch):
     dq = q.describe()
     q.close()
     assert dq["inflight"] == 3 and dq["prod_streams"] == 3 and dq["streams"] > 4, dq
+
+
+def test_pipeline_latches_dense_arith():
+    """A pipeline keeps the dense arithmetic it was created under
+    (asr_set_dense_arith changes the process-wide setting for later calls
+    only): batches submitted and collected after a switch to fp32 are the
+    split-bf16 production's bits, equal to a sequential split-bf16 decode;
+    a pipeline created after the switch runs fp32 and its emissions differ."""
+    T, B, inp, H, V, beam = 24, 600, 64, 256, 29, 30
+    W = _weights(inp, H, V, seed=17)
+    x = asr.DeviceMatrix.from_numpy(np.random.default_rng(9).uniform(-1, 1, (T * B, inp)).astype(np.float32))
+    assert asr.get_dense_arith() == asr.DENSE_SPLIT_BF16
+    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
+    em_split = asr.DeviceMatrix(T * B, V)
+    asr.model_emissions(x, W, T, B, em_split, True, recurrence=asr.RNN_RECUR_MFMA)
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    p.submit(x)
+    asr.set_dense_arith(asr.DENSE_F32)
+    try:
+        p.submit(x)
+        got = []
+        while p.pending():
+            lab, ln, lp, _ = p.collect()
+            got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+        assert np.array_equal(p.peek_emissions(), em_split.toCpu().reshape(T, B, V))
+        p.close()
+        for g in got:
+            assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+        q = asr.Pipeline(T, B, inp, H, V, beam, W)
+        q.submit(x)
+        q.collect()
+        assert not np.array_equal(q.peek_emissions(), em_split.toCpu().reshape(T, B, V))
+        q.close()
+    finally:
+        asr.set_dense_arith(asr.DENSE_SPLIT_BF16)
