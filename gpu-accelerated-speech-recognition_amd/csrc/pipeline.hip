@@ -496,14 +496,14 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // as many batches decoding at once as fill the decode CUs at the
         // one-wave kernel's occupancy (16 per CU at beam <= 56, ~9 at 100)
         const int Dw = std::max(1, std::min(8, (occw * dc + c.B / 2) / c.B));
-        // On the split-bf16 production (beam <= 56) one more decode is queued
-        // than the decode CUs hold: its workgroups start in the CUs the
-        // oldest decode's last utterances free, instead of after the host
-        // queues it (20 / 5, decodes in flight Dw / Dw + 1: 1024 per GPU 270.0 /
-        // 304.4 M frames/s, 512 242.4 / 259.5 M, 256 188.3 / 190.0 M, C4 as
-        // two 1024 batches 293.4 / 320.5 M; Dw + 2: 302.1 / 259.4 / — / 332.3 M;
-        // profiles/r04/bench_scan.md)
-        p->D = c.inflight ? c.inflight : (x3 && kcap <= 64 ? std::min(9, Dw + 1) : Dw);
+        // On the split-bf16 production (beam <= 56) two more decodes are
+        // queued than the decode CUs hold: their workgroups start in the CUs
+        // the oldest decodes' last utterances free, instead of after the host
+        // queues them (20 / 5, decodes in flight Dw / Dw + 1 / Dw + 2: C4 as
+        // two 1024 batches 293.4 / 320.6 / 330.2 M frames/s, 1024 per GPU
+        // 270.0 / 304.4 / 300.3 M, 512 242.4 / 259.5 / 255.9 M, 256 188.3 /
+        // 196.6 / 210.3 M; profiles/r04/bench_scan.md)
+        p->D = c.inflight ? c.inflight : (x3 && kcap <= 64 ? std::min(10, Dw + 2) : Dw);
         // production streams: the recurrence of a batch is latency-bound
         // (T steps) on B / 16 CUs, so as many batches produce at once as
         // decode at once (small shards: 256 per GPU, D = 8 -> P = 8)
