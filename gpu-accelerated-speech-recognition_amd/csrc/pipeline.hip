@@ -67,6 +67,7 @@ struct asr_pipeline {
     const float *W_out = nullptr, *b_out = nullptr;
     int ncu = 0, mode = SHARED, D = 1, P = 1, nbuf = 2, gcu = 0, dcus = 0, rnn_kind = -1;
     int arith = -1;       // the dense arithmetic latched at creation (asr_internal_dense_arith)
+    int ngroups = 1;      // CU groups of the decodes (GROUPS / GROUPS2): decode d on group d % ngroups
     bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
     bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
@@ -564,7 +565,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             p->fuse = c.V <= 32 && !(fe && fe[0] == '0');
         }
     }
-    if (p->mode != SHARED && p->D > 1 && (p->D + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
+    // CU groups (GROUPS / GROUPS2): decode d runs on group d % ngroups, so an
+    // explicit inflight beyond the groups queues decodes behind a group's
+    // current one.  Not the default: one or two queued decodes measured
+    // slower here (C2 50.8 -> 42.5 / 47.4 M frames/s, C5 3.37 -> 1.54 /
+    // 1.39 M; profiles/r04/bench_scan.md), unlike the chip-filling mode.
+    if (p->mode != SHARED && p->gcu) p->ngroups = std::max(1, std::min(p->D, ncu / p->gcu - 1));
+    if (p->mode != SHARED && p->D > 1 && (p->ngroups + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
     // T-segments (fused production only): explicit, ASR_PIPELINE_SEGMENTS
     // (A/B), else 2 for small shards (under 512 utterances: the job's fill
     // and drain are a large part of it; measured at 256 per GPU, 20 steps:
@@ -609,8 +616,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         if (p->grows > 0) mk(&p->s_gdec, 0, p->dcus);
     } else {
         for (int d = 0; d < p->D; d++)
-            mk(&p->s_dec[d], p->gcu ? d * p->gcu : 0, p->gcu ? (d + 1) * p->gcu : ncu);
-        for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->gcu ? p->D * p->gcu : 0, ncu);
+            mk(&p->s_dec[d], p->gcu ? (d % p->ngroups) * p->gcu : 0, p->gcu ? (d % p->ngroups + 1) * p->gcu : ncu);
+        for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->gcu ? p->ngroups * p->gcu : 0, ncu);
         if (p->split) mk(&p->s_gemm, 0, ncu);   // the GEMMs on every CU
     }
     // buffers, decoders, events
