@@ -125,7 +125,8 @@ int asr_rnn_recur_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_i
 /* Recurrence kernel choice for H <= 256 (H % 16 == 0), process-wide:
  * ASR_RNN_RECUR_VALU — one utterance per CU, W_hh in registers: the shortest
  *   step (~0.7-0.9 us), a whole CU per utterance;
- * ASR_RNN_RECUR_MFMA — 16 utterances per workgroup on MFMA: ~4.6 us per step
+ * ASR_RNN_RECUR_MFMA — 16 utterances per workgroup on MFMA: ~2.7 us per step
+ *   on the split-bf16 arithmetic at H = 256 (~4.6 us on fp32 MFMA)
  *   but ~3x less CU time per utterance (for throughput pipelines whose
  *   production runs beside other work);
  * ASR_RNN_RECUR_AUTO (default) — MFMA from B >= 4 x CUs on.
