@@ -1050,6 +1050,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             "inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
             "decode_cus": desc["decode_cus"], "fused_emission": fused,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
+            "segments": desc.get("segments"),
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "

@@ -577,9 +577,16 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // and drain are a large part of it; measured at 256 per GPU, 20 steps:
     // 1 / 2 / 4 segments 132.5 / 136.4 / 134.7 M frames/s), 1 otherwise
     // (2048 per GPU: 206.7 vs 201.6 M at 2; profiles/r04/bench_scan.md)
+    // On the split-bf16 production, 2 at every batch size (20 / 5, 1 / 2
+    // segments: C4 as two 1024 batches 330.8 / 335.0 M frames/s, 1024 per GPU
+    // 301.3 / 316.4 M, 512 256.4 / 259.0 M (268.9 at 4), 256 196.8 / 211.3 M
+    // (202.8 at 4): with decodes queued behind the resident ones a segment
+    // boundary no longer idles the decode CUs, and the last batch's decode
+    // starts T/2 recurrence steps earlier).
     if (p->fuse && p->mode == SHARED) {
         const char* se = getenv("ASR_PIPELINE_SEGMENTS");
-        int S = c.segments ? c.segments : (se ? atoi(se) : (c.B < 512 ? 2 : 1));
+        const int Sauto = (c.B < 512 || (asr::dense_x3_on() && kcap <= 64)) ? 2 : 1;
+        int S = c.segments ? c.segments : (se ? atoi(se) : Sauto);
         p->S = std::max(1, std::min(S, c.T));
     }
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
