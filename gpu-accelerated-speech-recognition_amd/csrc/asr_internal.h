@@ -35,6 +35,7 @@ extern thread_local int asr_internal_rnn_kind;
 // Set by the pipeline around GEMMs that share CUs with decodes: use the tiled
 // kernel (short-lived workgroups) instead of the persistent wide one, so that
 // a decode launched meanwhile waits at most one tile for its CUs.  Same bits.
+// The value is the split-bf16 kernel's row tiles per workgroup (0: off).
 extern thread_local int asr_internal_gemm_tiled;
 // Set by the pipeline around its productions: capture the per-frame
 // recurrence launches (H > 256) into the library's HIP graph at their first

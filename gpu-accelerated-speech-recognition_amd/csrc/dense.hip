@@ -469,8 +469,8 @@ int gemm_launch(const GemmArgs& g, int epi, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return ASR_ERR_ARG;
     // fp32-accurate split-bf16 kernel (dense_x3.hip) for the shapes it takes;
     // the pipeline's short-workgroup request (asr_internal_gemm_tiled) runs it
-    // in 8-tile runs instead of persistent workgroups
-    if (dense_x3_on() && gemm_x3_applies(g, epi)) return gemm_x3_launch(g, epi, asr_internal_gemm_tiled ? 8 : 0, s);
+    // in runs of that many row tiles instead of persistent workgroups
+    if (dense_x3_on() && gemm_x3_applies(g, epi)) return gemm_x3_launch(g, epi, asr_internal_gemm_tiled, s);
     if (epi == EPI_LOGSOFTMAX && g.N > 64) {
         // Rows wider than one workgroup tile (e.g. C5's V = 1000): bias GEMM,
         // then a row-wise log_softmax pass in place (model.py:49).

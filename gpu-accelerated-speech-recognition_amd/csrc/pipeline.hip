@@ -71,7 +71,7 @@ struct asr_pipeline {
     bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
     bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
-    bool gtiled = false;  // ... with the tiled GEMM kernel (several decodes in flight)
+    int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
     int G = 1;            // GROUPS2: batches whose recurrences run as one (a production group)
     std::vector<long> group;          // batches whose input projection is queued, recurrence not yet
@@ -82,6 +82,13 @@ struct asr_pipeline {
     std::vector<asr_ctc_t*> dec;
     std::vector<hipStream_t> s_dec, s_prod;
     hipStream_t s_gemm = nullptr;
+    // split production: the emission GEMMs on a stream of their own, so that
+    // the next batch's input GEMM does not queue behind the previous batch's
+    // emission GEMM, which waits for that batch's whole recurrence (C2: the
+    // recurrence stalled 65-150 us per batch for its input); s_gemm itself
+    // when the hardware queues are short
+    hipStream_t s_tail = nullptr;
+    bool tail_own = false;
     std::vector<hipEvent_t> ev_ready, ev_free, ev_proj, ev_rec;
     long submitted = 0, decoded = 0, collected = 0;
     long pending_tail = -1;   // split production: batch whose emission GEMM and decode are not queued yet
@@ -179,7 +186,7 @@ int produce_fused_segments(asr_pipeline* p, long i, const float* x, hipStream_t 
         const long r0 = (long)t0 * c.B, rows = (long)(t1 - t0) * c.B;
         const long ga = frac128 > 0 ? std::min(rows, frac128 * rows / ((long)c.T * c.B) / 128 * 128) : 0;
         if (ga > 0) {
-            asr_internal_gemm_tiled = p->gtiled ? 1 : 0;
+            asr_internal_gemm_tiled = p->gtiled;
             rc = asr_linear_fwd(x + r0 * c.in, p->W_ih, nullptr, p->hid[k] + r0 * c.H, (int)ga, c.in, c.H,
                                 ASR_EPI_NONE, p->s_gdec);
             asr_internal_gemm_tiled = 0;
@@ -225,7 +232,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
         // with several decodes in flight the decode-side rows use the tiled
         // kernel: a decode launched meanwhile then waits at most one tile's
         // workgroups for its CUs, not a persistent workgroup's whole share
-        asr_internal_gemm_tiled = p->gtiled ? 1 : 0;
+        asr_internal_gemm_tiled = p->gtiled;
         rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], (int)ga, c.in, c.H, ASR_EPI_NONE, p->s_gdec);
         asr_internal_gemm_tiled = 0;
         if (rc) return rc;
@@ -249,7 +256,12 @@ int produce_head(asr_pipeline* p, long i, const float* x) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
     if (fault(p, i, "head")) return ASR_ERR_INTERNAL;
+    // hid[k]'s previous batch: its emission GEMM has read it (stream order
+    // when both GEMMs share s_gemm)
+    if (p->tail_own) ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_ready[k], 0));
+    asr_internal_gemm_tiled = p->gtiled;
     int rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], c.T * c.B, c.in, c.H, ASR_EPI_NONE, p->s_gemm);
+    asr_internal_gemm_tiled = 0;
     if (rc) return rc;
     ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gemm));
     ASR_HIP_TRY(hipStreamWaitEvent(p->s_prod[0], p->ev_proj[k], 0));
@@ -267,12 +279,12 @@ int produce_tail(asr_pipeline* p, long i) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
     if (fault(p, i, "tail")) return ASR_ERR_INTERNAL;
-    ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_rec[k], 0));
-    ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_free[k], 0));
+    ASR_HIP_TRY(hipStreamWaitEvent(p->s_tail, p->ev_rec[k], 0));
+    ASR_HIP_TRY(hipStreamWaitEvent(p->s_tail, p->ev_free[k], 0));
     int rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
-                            ASR_EPI_BIAS_LOGSOFTMAX, p->s_gemm);
+                            ASR_EPI_BIAS_LOGSOFTMAX, p->s_tail);
     if (rc) return rc;
-    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], p->s_gemm));
+    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], p->s_tail));
     return ASR_OK;
 }
 
@@ -404,6 +416,7 @@ void release(asr_pipeline* p) {
     for (auto s : p->s_dec) if (s) hipStreamSynchronize(s);
     for (auto s : p->s_prod) if (s) hipStreamSynchronize(s);
     if (p->s_gemm) hipStreamSynchronize(p->s_gemm);
+    if (p->tail_own && p->s_tail) hipStreamSynchronize(p->s_tail);
     if (p->s_gdec) hipStreamSynchronize(p->s_gdec);
     for (auto h : p->dec) asr_ctc_destroy(h);
     for (auto b : p->hid) hipFree(b);
@@ -415,6 +428,7 @@ void release(asr_pipeline* p) {
     for (auto s : p->s_dec) if (s) hipStreamDestroy(s);
     for (auto s : p->s_prod) if (s) hipStreamDestroy(s);
     if (p->s_gemm) hipStreamDestroy(p->s_gemm);
+    if (p->tail_own && p->s_tail) hipStreamDestroy(p->s_tail);
     if (p->s_gdec) hipStreamDestroy(p->s_gdec);
 }
 
@@ -463,6 +477,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->D = c.inflight ? c.inflight : std::max(1, std::min(3, ncu / bcu - 1));
         p->P = 1;
         p->split = true;
+        const char* gt = getenv("ASR_PIPELINE_GTILED");
+        p->gtiled = gt ? std::max(0, atoi(gt)) : 0;
     } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 128 && 2 * bcu > ncu &&
                (occw = wave_occupancy(c)) > 0) {
         p->mode = SHARED;
@@ -532,8 +548,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             // 236 M, 240 M at 0.1)
             const double f = ge ? atof(ge) : (kcap > 64 || x3 ? 0.0 : 0.3);
             p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
-            const char* gt = getenv("ASR_PIPELINE_GTILED");   // A/B: 1 / 0 force, default: D > 1
-            p->gtiled = gt ? atoi(gt) != 0 : p->D > 1;
+            const char* gt = getenv("ASR_PIPELINE_GTILED");   // A/B: tiles per workgroup, 0 = persistent
+            p->gtiled = gt ? std::max(0, atoi(gt)) : (p->D > 1 ? 8 : 0);
         }
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
@@ -603,7 +619,9 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         while (nstreams() > p->hw_queues && !c.prod_streams && p->P > 1) p->P--;
         if (nstreams() > p->hw_queues && p->grows > 0) p->grows = 0;
         while (nstreams() > p->hw_queues && !c.inflight && p->D > 1) p->D--;
-        p->streams = nstreams();
+        const char* ts = getenv("ASR_PIPELINE_TAIL_STREAM");   // A/B: 0 = the emission GEMMs on s_gemm
+        p->tail_own = p->split && nstreams() < p->hw_queues && !(ts && ts[0] == '0');
+        p->streams = nstreams() + (p->tail_own ? 1 : 0);
     }
     // D decoding + P producing (+1: split production queues the next input
     // projection before the previous batch's emission projection)
@@ -626,6 +644,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             mk(&p->s_dec[d], p->gcu ? (d % p->ngroups) * p->gcu : 0, p->gcu ? (d % p->ngroups + 1) * p->gcu : ncu);
         for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->gcu ? p->ngroups * p->gcu : 0, ncu);
         if (p->split) mk(&p->s_gemm, 0, ncu);   // the GEMMs on every CU
+        if (p->tail_own) mk(&p->s_tail, 0, ncu);
+        else p->s_tail = p->s_gemm;
     }
     // buffers, decoders, events
     const size_t nh = (size_t)c.T * c.B * c.H, ne = (size_t)c.T * c.B * c.V;
