@@ -505,7 +505,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // On the split-bf16 arithmetic (dense_x3.hip) production costs ~half
         // the CU time, and half of the CUs decode at every batch size (256
         // per GPU, GSPLIT 0: 96 / 112 / 128 decode CUs 162 / 188 / 186 M
-        // frames/s; profiles/r04/bench_scan.md).
+        // frames/s; C4: 120 / 128 / 144 / 160 decode CUs 271 / 325 / 271 /
+        // 269 M, a sharp optimum at half; profiles/r04/bench_scan.md).
         const bool x3 = asr::dense_x3_on();
         const int dauto = (kcap > 64 || x3 ? ncu / 2 : (c.B < 512 ? ncu * 3 / 8 : ncu / 2)) / 8 * 8;
         p->dcus = part ? (c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : dauto) : 0;
