@@ -415,15 +415,6 @@ static bool try_gemm_wide(const GemmArgs& g, hipStream_t s, int& rc) {
     return true;
 }
 
-// ASR_GEMM_NARROW=0: the tiled kernel for narrow outputs too (A/B runs).
-static bool narrow_off() {
-    static const bool off = [] {
-        const char* e = getenv("ASR_GEMM_NARROW");
-        return e && e[0] == '0';
-    }();
-    return off;
-}
-
 template <int BN, int BK, int EPI>
 static int launch_gemm_bk(const GemmArgs& g, hipStream_t s) {
     const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
@@ -458,7 +449,7 @@ template <int EPI>
 static int launch_gemm_epi(const GemmArgs& g, hipStream_t s) {
     // the A stream as float4 rows: narrow outputs take the LDS-free A path
     const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
-    if (EPI != EPI_DUAL_TANH && g.N <= 64 && va && !narrow_off()) return launch_gemm_narrow<EPI>(g, s);
+    if (EPI != EPI_DUAL_TANH && g.N <= 64 && va) return launch_gemm_narrow<EPI>(g, s);
     int rc;
     if (try_gemm_wide<EPI>(g, s, rc)) return rc;
     if (g.N <= 32) return launch_gemm_bn<32, EPI>(g, s);
@@ -600,12 +591,8 @@ int rnn_recur_launch(const float* h0, const float* Whh, const float* b_ih, const
                      float* hid, int T, int B, int H, hipStream_t s) {
     if (H > RNN_HMAX) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H * 4 > 0x7fffffe0L) return ASR_ERR_UNSUPPORTED;   // one step's rows per buffer resource
-    // packed FMAs (two k per instruction) unless ASR_RNN_PK=0 (A/B)
-    static const bool pk = [] { const char* e = getenv("ASR_RNN_PK"); return !e || atoi(e) != 0; }();
-    if (pk)
-        hipLaunchKernelGGL(rnn_recur_kernel<true>, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid, T, B, H);
-    else
-        hipLaunchKernelGGL(rnn_recur_kernel<false>, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid, T, B, H);
+    // packed FMAs (two k per instruction)
+    hipLaunchKernelGGL(rnn_recur_kernel<true>, dim3(B), dim3(1024), 0, s, h0, Whh, b_ih, b_hh, hid, T, B, H);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }

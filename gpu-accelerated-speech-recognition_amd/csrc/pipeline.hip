@@ -130,8 +130,7 @@ void set_failed(asr_pipeline* p, long from, int rc) {
 }
 
 int cu_stream(hipStream_t* s, int ncu, int lo, int hi) {
-    static const int mask_all = [] { const char* e = getenv("ASR_PIPELINE_MASKALL"); return e ? atoi(e) : 0; }();
-    if (lo <= 0 && hi >= ncu && !mask_all) {
+    if (lo <= 0 && hi >= ncu) {
         ASR_HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         return ASR_OK;
     }
@@ -477,8 +476,6 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->D = c.inflight ? c.inflight : std::max(1, std::min(3, ncu / bcu - 1));
         p->P = 1;
         p->split = true;
-        const char* gt = getenv("ASR_PIPELINE_GTILED");
-        p->gtiled = gt ? std::max(0, atoi(gt)) : 0;
     } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 128 && 2 * bcu > ncu &&
                (occw = wave_occupancy(c)) > 0) {
         p->mode = SHARED;
@@ -526,12 +523,10 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // (T steps) on B / 16 CUs, so as many batches produce at once as
         // decode at once (small shards: 256 per GPU, D = 8 -> P = 8)
         p->P = c.prod_streams ? c.prod_streams : (part ? std::max(3, p->D) : 1);
-        // the fused recurrence + emission kernel (ASR_PIPELINE_FUSE=0: the
-        // recurrence and the emission GEMM separately, A/B), and the decode
-        // CUs' share of the input projection rows (ASR_PIPELINE_GSPLIT: a
-        // fraction of the rows, A/B)
-        const char* fe = getenv("ASR_PIPELINE_FUSE");
-        p->fuse = (c.H & 15) == 0 && c.V <= 32 && !(fe && fe[0] == '0');
+        // the fused recurrence + emission kernel, and the decode CUs' share
+        // of the input projection rows (ASR_PIPELINE_GSPLIT: a fraction of
+        // the rows, A/B)
+        p->fuse = (c.H & 15) == 0 && c.V <= 32;
         if (p->fuse && p->dcus) {
             const char* ge = getenv("ASR_PIPELINE_GSPLIT");
             // default 0.3 (measured, C4 one GPU: 0 / 0.2 / 0.3 / 0.4 / 0.5 ->
@@ -549,8 +544,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             // 236 M, 240 M at 0.1)
             const double f = ge ? atof(ge) : (kcap > 64 || x3 ? 0.0 : 0.3);
             p->grows = (long)(std::max(0.0, std::min(1.0, f)) * c.T * c.B) / 128 * 128;
-            const char* gt = getenv("ASR_PIPELINE_GTILED");   // A/B: tiles per workgroup, 0 = persistent
-            p->gtiled = gt ? std::max(0, atoi(gt)) : (p->D > 1 ? 8 : 0);
+            p->gtiled = p->D > 1 ? 8 : 0;
         }
     } else if (4 * bcu <= ncu) {   // small batches otherwise (C5: H = 1024, V = 1000)
         p->mode = GROUPS2;
@@ -578,8 +572,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->P = c.prod_streams ? c.prod_streams : 2;
         if (c.H <= 256 && (c.H & 15) == 0) {
             p->rnn_kind = ASR_RNN_RECUR_MFMA;
-            const char* fe = getenv("ASR_PIPELINE_FUSE");
-            p->fuse = c.V <= 32 && !(fe && fe[0] == '0');
+            p->fuse = c.V <= 32;
         }
     }
     // CU groups (GROUPS / GROUPS2): decode d runs on group d % ngroups, so an
@@ -589,8 +582,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // 1.39 M; profiles/r04/bench_scan.md), unlike the chip-filling mode.
     if (p->mode != SHARED && p->gcu) p->ngroups = std::max(1, std::min(p->D, ncu / p->gcu - 1));
     if (p->mode != SHARED && p->D > 1 && (p->ngroups + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
-    // T-segments (fused production only): explicit, ASR_PIPELINE_SEGMENTS
-    // (A/B), else 2 for small shards (under 512 utterances: the job's fill
+    // T-segments (fused production only): explicit (config.segments), else 2 for small shards (under 512 utterances: the job's fill
     // and drain are a large part of it; measured at 256 per GPU, 20 steps:
     // 1 / 2 / 4 segments 132.5 / 136.4 / 134.7 M frames/s), 1 otherwise
     // (2048 per GPU: 206.7 vs 201.6 M at 2; profiles/r04/bench_scan.md)
@@ -601,9 +593,8 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // boundary no longer idles the decode CUs, and the last batch's decode
     // starts T/2 recurrence steps earlier).
     if (p->fuse && p->mode == SHARED) {
-        const char* se = getenv("ASR_PIPELINE_SEGMENTS");
         const int Sauto = (c.B < 512 || (asr::dense_x3_on() && kcap <= 64)) ? 2 : 1;
-        int S = c.segments ? c.segments : (se ? atoi(se) : Sauto);
+        const int S = c.segments ? c.segments : Sauto;
         p->S = std::max(1, std::min(S, c.T));
     }
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
@@ -620,8 +611,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         while (nstreams() > p->hw_queues && !c.prod_streams && p->P > 1) p->P--;
         if (nstreams() > p->hw_queues && p->grows > 0) p->grows = 0;
         while (nstreams() > p->hw_queues && !c.inflight && p->D > 1) p->D--;
-        const char* ts = getenv("ASR_PIPELINE_TAIL_STREAM");   // A/B: 0 = the emission GEMMs on s_gemm
-        p->tail_own = p->split && nstreams() < p->hw_queues && !(ts && ts[0] == '0');
+        p->tail_own = p->split && nstreams() < p->hw_queues;
         p->streams = nstreams() + (p->tail_own ? 1 : 0);
     }
     // D decoding + P producing (+1: split production queues the next input

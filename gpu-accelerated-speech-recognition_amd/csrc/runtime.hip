@@ -492,7 +492,7 @@ struct asr_ctc {
     // pinned host mirrors of the best-path results
     unsigned char* h_res = nullptr;   // pinned mirror of d_res
     unsigned char* hd_res = nullptr;  // h_res as the device sees it (the kernels write there directly)
-    bool res_direct = true;           // kernels write results into h_res (ASR_CTC_RESULT_COPY=1: copy d_res)
+    bool res_direct = true;           // kernels write results into h_res (else: copy d_res)
     int *h_best_lab = nullptr, *h_best_len = nullptr, *h_status = nullptr;
     double* h_best_score = nullptr;
     // last decode
@@ -726,7 +726,6 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
     if (const char* t0 = getenv("ASR_CTC_TILE0")) h->tile0 = atoi(t0) != 0;
     if (const char* fb = getenv("ASR_CTC_WIDE_FALLBACK")) h->diag = atoi(fb) != 0 ? 1 : 0;
-    if (const char* rc_ = getenv("ASR_CTC_RESULT_COPY")) h->res_direct = atoi(rc_) == 0;
     if (asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }
