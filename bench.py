@@ -847,6 +847,14 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
         wl = args.config + (" decode-only" if args.decode_only else "")
         traffic = load_counters("traffic", wl, variant)
         issue = load_counters("issue", wl, variant)
+        # a T-segmented decode (asr_pipeline segments) is S kernel dispatches
+        # of T / S frames each; a "launch" here is the whole decode of a
+        # batch (the HIP-event spans of its dispatches, summed), so the
+        # per-dispatch counter and trace figures are scaled by S
+        nseg = int((sched or {}).get("segments") or 1)
+        kstats = load_kernel_stats(wl, variant)
+        if kstats:
+            kstats = dict(kstats, dispatches_per_launch=nseg, per_launch_ms=round(kstats["avg_ms"] * nseg, 4))
         # The decoder moves ~4V + 8 bytes per live node per frame: the beam
         # never leaves the CU, so HBM is not what bounds it.  Its limiter is
         # the per-frame dependency chain on chip (LDS round trips, barriers,
@@ -857,13 +865,14 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                 "frac_of": "HBM roofline (SURVEY §8(d) algorithmic bytes: 4V + 40K per frame)",
                 "avg_launch_ms": round(avg_kernel_ms, 4), "bytes_per_frame": bpf,
                 "frames_per_launch": Bl * T, "us_per_frame_step": round(1e3 * avg_kernel_ms / T, 4),
-                "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+                "decode_dispatches_per_launch": nseg,
+                "traffic": traffic["hbm_bytes_per_launch"] * nseg if traffic else None,
                 "traffic_source": traffic, "issue": issue,
                 # avg_launch_ms is the HIP-event span on the decode stream: with
                 # one decode queued beyond those the decode CUs hold it includes
                 # that decode's wait for CUs; rocprofv3's dispatch duration of
                 # the same kernel in the committed trace of this workload:
-                "rocprof_kernel": load_kernel_stats(wl, variant),
+                "rocprof_kernel": kstats,
                 "limiter": "on-chip dependency latency per frame (beam resident in LDS): "
                            "see roofline.issue for the measured issue/wait fractions"}
 
