@@ -398,8 +398,10 @@ int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode
  * streams round-robin onto the queues and streams that share a queue
  * serialise, so the automatic schedule is fitted to the queues (fewer
  * production streams, then no input-projection share on the decode CUs,
- * then fewer decodes in flight); streams > hw_queues only when the caller
- * fixed inflight / prod_streams.  DESIGN.md §7c gives the measured cost. */
+ * then fewer decodes in flight; the small-batch mode's emission GEMMs get
+ * a stream of their own only when a queue is left for it); streams >
+ * hw_queues only when the caller fixed inflight / prod_streams.  DESIGN.md
+ * §7c gives the measured cost. */
 int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues);
 /* The emissions [T][B][V] (log-probabilities, device) that the decode of the
  * batch last returned by asr_pipeline_collect consumed — the exact bytes, for
