@@ -375,6 +375,9 @@ def main():
                     help="batches decoded concurrently, each on its own HIP stream and CU group "
                          "(0 = auto: as many one-CU-per-utterance groups as fit beside production, "
                          "at most 3; 1 = one decode at a time)")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="T-segments per batch handed from production to decode (native pipeline, "
+                         "fused production; 0 = the library's choice)")
     ap.add_argument("--decode-cus", type=int, default=0,
                     help="CUs per decode group (0: one per utterance, B rounded up to 8); fewer "
                          "CUs than utterances puts several decode workgroups on a CU when their "
@@ -967,7 +970,8 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     else:
         xs = [d_x]
     pl = asr.Pipeline(T, Bp, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
-                      inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus)
+                      inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus,
+                      segments=args.segments)
     desc = pl.describe()
     if desc["mode"] == asr.PIPELINE_MODES[1] and H <= 256:
         # the pipeline's MFMA recurrence for chip-filling batches, also for
