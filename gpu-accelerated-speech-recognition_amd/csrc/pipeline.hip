@@ -591,9 +591,12 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // 301.3 / 316.4 M, 512 256.4 / 259.0 M (268.9 at 4), 256 196.8 / 211.3 M
     // (202.8 at 4): with decodes queued behind the resident ones a segment
     // boundary no longer idles the decode CUs, and the last batch's decode
-    // starts T/2 recurrence steps earlier).
+    // starts T/2 recurrence steps earlier); 4 for 512-1023 utterances
+    // (run c4s: 512 per GPU 264.2 / 271.6 M at 2 / 4; 1024 312.6 / 315.3 M
+    // and C4 332.6 / 323.3 M, within or below the noise; 256 211.3 / 202.8).
     if (p->fuse && p->mode == SHARED) {
-        const int Sauto = (c.B < 512 || (asr::dense_x3_on() && kcap <= 64)) ? 2 : 1;
+        const bool x3s = asr::dense_x3_on() && kcap <= 64;
+        const int Sauto = x3s && c.B >= 512 && c.B < 1024 ? 4 : (c.B < 512 || x3s) ? 2 : 1;
         const int S = c.segments ? c.segments : Sauto;
         p->S = std::max(1, std::min(S, c.T));
     }

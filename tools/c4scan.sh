@@ -1,15 +1,8 @@
 set -e
-mkdir -p gpurun_out/c4s
-run() { # name, args...
-  n=$1; shift
-  timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify "$@" > gpurun_out/c4s/$n.json 2>gpurun_out/c4s/$n.err
-  python -c "import json;d=json.load(open('gpurun_out/c4s/$n.json'));c=d['config'];print('$n', round(d['value']/1e6,2), d['ms_per_step'], c.get('segments'), c.get('inflight_decodes'))"
-}
-run c4_s2 --config C4
-run c4_s3 --config C4 --segments 3
-run c4_s4 --config C4 --segments 4
-run c4_s2_i5 --config C4 --inflight 5
-run g1024_s4 --config C4 --global-batch 1024 --segments 4
-run g512_s4 --config C4 --global-batch 512 --segments 4
-run g512_s2 --config C4 --global-batch 512
-run g1024_s3 --config C4 --global-batch 1024 --segments 3
+mkdir -p gpurun_out/c4t
+timeout -k 10 400 python -u -m pytest tests/test_pipeline_gpu.py tests/test_ctc_segment_gpu.py tests/test_full_configs_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/c4t/pytest.log 2>&1
+tail -1 gpurun_out/c4t/pytest.log
+for n in 512 256; do
+timeout -k 10 150 python bench.py --steps 20 --warmup 5 --config C4 --global-batch $n > gpurun_out/c4t/g$n.json 2>gpurun_out/c4t/g$n.err
+python -c "import json;d=json.load(open('gpurun_out/c4t/g$n.json'));c=d['config'];print('g$n', round(d['value']/1e6,2), d['ms_per_step'], c.get('segments'), (d.get('parity') or {}).get('match'))"
+done
