@@ -124,6 +124,13 @@ int wave_occupancy(const asr_pipeline_config& c) {
     return n;
 }
 
+// The automatic T-segment count of a fused chip-filling production (the
+// measurements are at asr_pipeline_create's use of it).
+int auto_segments(const asr_pipeline_config& c, int kcap) {
+    const bool x3s = asr::dense_x3_on() && kcap <= 64;
+    return x3s && c.B >= 512 && c.B < 1024 ? 4 : (c.B < 512 || x3s) ? 2 : 1;
+}
+
 void set_failed(asr_pipeline* p, long from, int rc) {
     if (p->fail_from < 0 || from < p->fail_from) p->fail_from = from;
     if (p->fail_rc == ASR_OK) p->fail_rc = rc;
@@ -518,7 +525,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // two 1024 batches 293.4 / 320.6 / 330.2 M frames/s, 1024 per GPU
         // 270.0 / 304.4 / 300.3 M, 512 242.4 / 259.5 / 255.9 M, 256 188.3 /
         // 196.6 / 210.3 M; profiles/r04/bench_scan.md)
-        p->D = c.inflight ? c.inflight : (x3 && kcap <= 64 ? std::min(10, Dw + 2) : Dw);
+        // With four T-segments per batch (512-1023 utterances, below) three
+        // (512 per GPU, 20 / 5, 6 / 7 / 8 decodes: 267.7-268.0 / 281.5-289.6
+        // / 278.1 M; 1024 and C4 at 2 segments: 4 / 5 decodes 310.2 / 305.5
+        // and 334.0-334.5 / 329.7-332.8 M; 256: 10 / 11 / 12 decodes 207.3 /
+        // 199.2 / 153.3 M; run c4d)
+        const int Sw = c.segments ? c.segments : auto_segments(c, kcap);
+        p->D = c.inflight ? c.inflight : (x3 && kcap <= 64 ? std::min(10, Dw + (Sw >= 4 ? 3 : 2)) : Dw);
         // production streams: the recurrence of a batch is latency-bound
         // (T steps) on B / 16 CUs, so as many batches produce at once as
         // decode at once (small shards: 256 per GPU, D = 8 -> P = 8)
@@ -595,9 +608,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // (run c4s: 512 per GPU 264.2 / 271.6 M at 2 / 4; 1024 312.6 / 315.3 M
     // and C4 332.6 / 323.3 M, within or below the noise; 256 211.3 / 202.8).
     if (p->fuse && p->mode == SHARED) {
-        const bool x3s = asr::dense_x3_on() && kcap <= 64;
-        const int Sauto = x3s && c.B >= 512 && c.B < 1024 ? 4 : (c.B < 512 || x3s) ? 2 : 1;
-        const int S = c.segments ? c.segments : Sauto;
+        const int S = c.segments ? c.segments : auto_segments(c, kcap);
         p->S = std::max(1, std::min(S, c.T));
     }
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
