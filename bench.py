@@ -69,6 +69,11 @@ if _hwq is not None:
 elif int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
+# c10's INFO lines (gloo's "[Gloo] Rank r is connected to n peer ranks") can
+# land on stdout before rank 0's JSON line: keep stdout to that one line.
+# Read when torch is imported, so set here, before the import.
+os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")
+
 try:
     import torch
     import torch.distributed as dist
@@ -276,6 +281,21 @@ def load_mfma_counters(workload: str):
     return None
 
 
+def init_gloo(rank: int, world: int) -> None:
+    """dist.init_process_group("gloo") with the native stdout (fd 1) pointed
+    at stderr meanwhile: gloo prints "[Gloo] Rank r is connected to n peer
+    ranks" to stdout from C++ while it connects, and rank 0's stdout must be
+    the one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def cpu_share():
     """Host cores this process may use: the affinity mask, capped by a cgroup
     CPU quota (a GPU box may show many more CPUs than its share), else
@@ -447,7 +467,7 @@ def main():
     ndev = torch.cuda.device_count() if torch is not None else 1
     local = local % max(1, ndev)
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_gloo(rank, world)
     asr.set_device(local)
 
     T, H, V, beam = cfg["T"], cfg["hidden"], cfg["vocab"], cfg["beam"]
@@ -1100,7 +1120,7 @@ def dry_run_cpu(cfg, rank, world):
     GB = cfg["global_batch"] if strong else cfg["batch"] * world
     first, B = shard_range(rank, world, GB) if strong else (shard_first(rank, cfg["batch"]), cfg["batch"])
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_gloo(rank, world)
         dist.barrier()
     t0 = time.perf_counter()
     lab, ln, lp = greedy_host(T, V, first, B)
