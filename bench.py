@@ -315,6 +315,134 @@ def cpu_share():
     return max(1, n), quota
 
 
+class ClockSampler:
+    """The GPU's shader (gfx) clock, socket power and hotspot temperature,
+    sampled every ~10 ms from the driver's gpu_metrics (amdsmi) in a
+    background thread over the timed region, so that a line measured on a
+    slower-clocked box says so.  None fields when amdsmi is unavailable."""
+
+    def __init__(self, local: int):
+        self.samples, self.err, self.h = [], None, None
+        self._stop = None
+        try:
+            import amdsmi
+            self.amdsmi = amdsmi
+            amdsmi.amdsmi_init()
+            handles = amdsmi.amdsmi_get_processor_handles()
+            want = None
+            try:   # match torch's device by PCI bus id
+                pr = torch.cuda.get_device_properties(local)
+                want = (int(pr.pci_domain_id), int(pr.pci_bus_id), int(pr.pci_device_id))
+            except Exception:
+                pass
+            for h in handles:
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)   # "dddd:bb:dd.f"
+                dom, bus, rest = bdf.split(":")
+                dev = rest.split(".")[0]
+                if want is None or (int(dom, 16), int(bus, 16), int(dev, 16)) == want:
+                    self.h = h
+                    break
+            if self.h is None and len(handles) == 1:
+                self.h = handles[0]
+            if self.h is None:
+                self.err = f"no amdsmi device matches the torch device ({len(handles)} visible)"
+        except Exception as e:  # pragma: no cover - depends on the box
+            self.err = f"amdsmi unavailable: {type(e).__name__}: {e}"
+
+    def _one(self):
+        m = self.amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+        def num(v):
+            try:
+                v = float(v)
+                return v if v < 65535 else None   # 0xFFFF: field not supported
+            except Exception:
+                return None
+        clk = m.get("current_gfxclk")
+        if num(clk) is None:   # per-XCD clocks (gpu_metrics v1.4+)
+            xs = [num(v) for v in (m.get("current_gfxclks") or [])]
+            xs = [v for v in xs if v]
+            clk = sum(xs) / len(xs) if xs else None
+        return (time.perf_counter(), num(clk), num(m.get("current_socket_power") or m.get("average_socket_power")),
+                num(m.get("temperature_hotspot")))
+
+    def start(self):
+        import threading
+        if self.h is None:
+            return
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.is_set():
+                try:
+                    self.samples.append(self._one())
+                except Exception as e:  # pragma: no cover
+                    self.err = f"{type(e).__name__}: {e}"
+                    return
+                self._stop.wait(0.01)
+        self._t = threading.Thread(target=loop, daemon=True)
+        self._t.start()
+
+    def stop(self):
+        if self._stop is not None:
+            self._stop.set()
+            self._t.join()
+        try:
+            if self.h is not None:
+                self.amdsmi.amdsmi_shut_down()
+        except Exception:
+            pass
+        clk = [c for _, c, _, _ in self.samples if c]
+        pw = [w for _, _, w, _ in self.samples if w]
+        tp = [t for _, _, _, t in self.samples if t]
+        if not clk:
+            return {"source": "amdsmi gpu_metrics", "samples": len(self.samples), "gfxclk_mhz": None,
+                    "error": self.err}
+        return {"source": "amdsmi gpu_metrics (current_gfxclk), every ~10 ms over the timed region",
+                "samples": len(self.samples), "gfxclk_mhz": {"mean": round(float(np.mean(clk)), 1),
+                                                             "min": round(float(min(clk)), 1),
+                                                             "max": round(float(max(clk)), 1)},
+                "socket_power_w": round(float(np.mean(pw)), 1) if pw else None,
+                "hotspot_c_max": round(float(max(tp)), 1) if tp else None}
+
+
+def union_ms(iv):
+    """Total length of the union of intervals [(a, b)]."""
+    tot, end = 0.0, None
+    for a, b in sorted(iv):
+        if end is None or a > end:
+            tot += b - a
+            end = b
+        elif b > end:
+            tot += b - end
+            end = b
+    return tot
+
+
+def stage_figures(stamps, elapsed_ms, host_wait_ms, steps, nsub):
+    """Per-stage figures of the timed region from the pipeline's timeline
+    (asr_pipeline_get_timeline: per batch, ms after the region's start, of
+    its production start / end and decode start / end) and the host's time
+    blocked in collect: what the step is made of."""
+    if stamps is None or len(stamps) == 0:
+        return None
+    t = np.asarray(stamps, np.float64)
+    prod, dec = t[:, 1] - t[:, 0], t[:, 3] - t[:, 2]
+    return {
+        "source": "HIP timing events recorded by the pipeline in the timed run (asr_pipeline_set_timing)",
+        "batches": int(len(t)),
+        "production_ms_per_batch": round(float(prod.mean()), 4),
+        "decode_span_ms_per_batch": round(float(dec.mean()), 4),
+        "production_busy_frac": round(union_ms(list(zip(t[:, 0], t[:, 1]))) / elapsed_ms, 4),
+        "decode_busy_frac": round(union_ms(list(zip(t[:, 2], t[:, 3]))) / elapsed_ms, 4),
+        "first_decode_start_ms": round(float(t[:, 2].min()), 4),
+        "last_production_end_ms": round(float(t[:, 1].max()), 4),
+        "last_decode_end_ms": round(float(t[:, 3].max()), 4),
+        "steady_ms_per_step": (round(float((t[-1, 3] - t[nsub - 1, 3]) / (steps - 1)), 4) if steps > 1 else None),
+        "host_wait_ms_per_step": round(host_wait_ms / steps, 4),
+        "note": "a decode's start is when its stream reached it (it may then wait for CUs); steady_ms_per_step "
+                "= decode ends of the first to the last step over steps - 1 (no fill, no drain)"}
+
+
 def cpu_model() -> str:
     try:
         for line in Path("/proc/cpuinfo").read_text().splitlines():
@@ -381,6 +509,9 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--decode-only", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timeline", action="store_true",
+                    help="native pipeline: no per-batch timing events in the timed run (the line's "
+                         "config.stages is then null)")
     ap.add_argument("--cpu-full-T", action="store_true",
                     help="CPU baseline / parity sample over all T frames at any shape (default: all of "
                          "them when that is ~20 s of CPU work, as at C4; a prefix otherwise)")
@@ -933,6 +1064,9 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                            best_p, full_T=args.cpu_full_T, emis_note=note)
         parity = cpu.pop("parity")
 
+    # per-stage spans, clock and CU placement of the timed run: top-level fields of the line
+    sched = dict(sched or {})
+    measured = {k: sched.pop(k) for k in ("stages", "clock", "cu_placement") if k in sched}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
@@ -954,6 +1088,7 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                        "dense_arith": "split_bf16" if asr.get_dense_arith() == asr.DENSE_SPLIT_BF16 else "f32",
                        **sched},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "parity": parity, "gather": gather,
+            **measured,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -1011,7 +1146,9 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     slots = [(np.empty_like(_l), np.empty_like(_n), np.empty_like(_p)) for _ in range(nsub)]
 
     def take():
+        tw = time.perf_counter()
         lab, ln, lp, ms = pl.collect(out=slots[take.j % nsub])
+        take.wait += time.perf_counter() - tw
         take.j += 1
         kernel_ms.append(ms)
         if hostlog is not None:
@@ -1029,20 +1166,43 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             take()
     run.k = 0
     take.j = 0
+    take.wait = 0.0
 
     run(-(-(2 * (desc["inflight"] + desc["prod_streams"]) + 1) // nsub))   # every buffer, stream and workspace once
     run(args.warmup)
     kernel_ms.clear()
+    timeline = not args.no_timeline
+    clock = ClockSampler(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     if world > 1:
         dist.barrier()
     gc.collect()
     gc.disable()
     asr.synchronize()
+    if timeline:   # per-batch stage stamps of the timed run (4 timing events per batch), from now
+        pl.set_timing(True)
+    clock.start()
+    take.wait = 0.0
     t0 = time.perf_counter()
     run(args.steps)
     asr.synchronize()
     elapsed = time.perf_counter() - t0
+    clock_fig = clock.stop()
     gc.enable()
+    stages = None
+    if timeline:
+        _, stamps = pl.timeline()
+        stages = stage_figures(stamps, 1e3 * elapsed, 1e3 * take.wait, args.steps, nsub)
+        if os.environ.get("ASR_BENCH_TIMELINE"):   # diagnostics: the raw per-batch stamps
+            np.savetxt(os.environ["ASR_BENCH_TIMELINE"], stamps, fmt="%.4f",
+                       header="production start, production end, decode start, decode end (ms)")
+        pl.set_timing(False)
+    placement = {"streams": [list(r) for r in pl.placement()]}
+    try:   # physical CUs per XCD that each role's CU mask reaches (HW_REG_XCC_ID / HW_ID probe)
+        for role in ("decode", "production"):
+            if any(r[0] == role for r in placement["streams"]):
+                placement[role + "_cus_per_xcd"] = pl.probe_placement(role)
+    except Exception as e:  # pragma: no cover
+        placement["probe_error"] = str(e)
     if hostlog is not None:
         with open(os.environ["ASR_BENCH_HOSTLOG"], "w") as f:
             for what, tt in hostlog:
@@ -1085,6 +1245,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
             "segments": desc.get("segments"),
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
+            "stages": stages, "clock": clock_fig, "cu_placement": placement,
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
                         f"library-owned streams, buffers and decoder schedule"},

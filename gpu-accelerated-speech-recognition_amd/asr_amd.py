@@ -60,8 +60,12 @@ EXPORTS = [
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
     "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams",
     "asr_pipeline_peek_emissions", "asr_pipeline_get_segments", "asr_pipeline_get_groups",
-    "asr_pipeline_destroy",
+    "asr_pipeline_get_placement", "asr_pipeline_probe_placement", "asr_pipeline_set_timing",
+    "asr_pipeline_get_timeline", "asr_pipeline_destroy",
 ]
+# asr_pipeline_get_placement roles (ASR_PIPE_ROLE_*)
+PIPE_ROLES = {0: "decode", 1: "production", 2: "decode_cu_gemm", 3: "gemm"}
+ASR_MAX_XCC = 16
 
 
 class AsrError(RuntimeError):
@@ -128,6 +132,12 @@ def lib() -> ctypes.CDLL:
         "asr_pipeline_get_production": [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_longlong),
                                         ctypes.POINTER(_i)],
         "asr_pipeline_get_streams": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)],
+        "asr_pipeline_get_placement": [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
+                                       ctypes.POINTER(_i)],
+        "asr_pipeline_probe_placement": [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)],
+        "asr_pipeline_set_timing": [_vp, _i],
+        "asr_pipeline_get_timeline": [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_longlong),
+                                      ctypes.POINTER(_f)],
         "asr_pipeline_peek_emissions": [_vp, ctypes.POINTER(_vp)],
         "asr_pipeline_get_segments": [_vp, ctypes.POINTER(_i)],
         "asr_pipeline_get_groups": [_vp, ctypes.POINTER(_i)],
@@ -625,6 +635,43 @@ class Pipeline:
                 "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
                 "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
                 "hw_queues": hq.value, "segments": sg.value, "groups": gp.value}
+
+    def placement(self):
+        """[(role name, cu_lo, cu_hi)] of every stream the pipeline created."""
+        n = _i()
+        check(lib().asr_pipeline_get_placement(self.h, 0, ctypes.byref(n), None, None, None),
+              "asr_pipeline_get_placement")
+        cnt = n.value
+        role, lo, hi = (_i * max(1, cnt))(), (_i * max(1, cnt))(), (_i * max(1, cnt))()
+        check(lib().asr_pipeline_get_placement(self.h, cnt, ctypes.byref(n), role, lo, hi),
+              "asr_pipeline_get_placement")
+        return [(PIPE_ROLES.get(role[i], role[i]), lo[i], hi[i]) for i in range(cnt)]
+
+    def probe_placement(self, role: str):
+        """Physical CUs per XCD that the first stream of `role` reaches (one
+        probe launch; synchronises that stream): a list, one count per XCD."""
+        r = {v: k for k, v in PIPE_ROLES.items()}[role]
+        cnt, nx = (_i * ASR_MAX_XCC)(), _i()
+        check(lib().asr_pipeline_probe_placement(self.h, r, cnt, ctypes.byref(nx)), "asr_pipeline_probe_placement")
+        return [cnt[i] for i in range(nx.value)]
+
+    def set_timing(self, on: bool = True) -> None:
+        """Record per-batch production / decode timing events from the next
+        submit on (call on a drained pipeline; clears the timeline)."""
+        check(lib().asr_pipeline_set_timing(self.h, 1 if on else 0), "asr_pipeline_set_timing")
+
+    def timeline(self):
+        """(batch ids [n], stamps [n, 4] ms: production start / end, decode
+        start / end) of the batches collected since set_timing."""
+        n = _i()
+        check(lib().asr_pipeline_get_timeline(self.h, 0, ctypes.byref(n), None, None), "asr_pipeline_get_timeline")
+        cnt = n.value
+        b = np.zeros(max(1, cnt), np.int64)
+        t = np.zeros((max(1, cnt), 4), np.float32)
+        check(lib().asr_pipeline_get_timeline(self.h, cnt, ctypes.byref(n),
+                                              b.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                                              t.ctypes.data_as(ctypes.POINTER(_f))), "asr_pipeline_get_timeline")
+        return b[:cnt], t[:cnt]
 
     def submit(self, x: "DeviceMatrix") -> None:
         """Queue a batch.  x is kept alive here until its batch is collected

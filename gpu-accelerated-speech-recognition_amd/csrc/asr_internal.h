@@ -26,6 +26,25 @@
 
 void asr_internal_set_error(const char* what, const char* msg, const char* file, int line);
 
+#include <mutex>
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) of one kernel, once per
+// device, safe under concurrent first calls (pipeline threads, several
+// devices in one process).  One static instance per kernel instantiation.
+struct AsrAttrOnce {
+    std::mutex m;
+    uint64_t done = 0;   // bit d: set on device d
+    int set(const void* fn, int bytes) {
+        int dev = 0;
+        ASR_HIP_TRY(hipGetDevice(&dev));
+        const uint64_t bit = (dev >= 0 && dev < 64) ? (1ull << dev) : 0ull;
+        std::lock_guard<std::mutex> g(m);
+        if (bit && (done & bit)) return ASR_OK;
+        ASR_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+        done |= bit;
+        return ASR_OK;
+    }
+};
+
 static inline hipStream_t asr_stream(asr_stream_t s) { return (hipStream_t)s; }
 
 // Recurrence kernel for this thread's next RNN calls (ASR_RNN_RECUR_*; -1:

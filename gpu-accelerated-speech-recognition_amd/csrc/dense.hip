@@ -372,12 +372,8 @@ __global__ __launch_bounds__(64 * GW_W) void gemm_wide_kernel(GemmArgs g) {
 template <int BNW, int KMAX, int EPI>
 static int launch_gemm_wide_k(const GemmArgs& g, hipStream_t s) {
     const size_t lds = sizeof(float) * (size_t)BNW * (KMAX + 4);
-    static bool attr = false;
-    if (!attr) {
-        ASR_HIP_TRY(hipFuncSetAttribute((const void*)gemm_wide_kernel<BNW, KMAX, EPI>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    static AsrAttrOnce attr;
+    if (int r_ = attr.set((const void*)gemm_wide_kernel<BNW, KMAX, EPI>, 160 * 1024)) return r_;
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
@@ -646,7 +642,7 @@ constexpr int RE_PART = (RNN_HMAX / 32) * RM_ROWS * RE_VMAX;   // EMIT: one buff
 // HL: also write h_{T-1} to hlast (segmented production); a separate
 // instance, so that the unsegmented kernel carries no extra state.
 template <bool EMIT, bool HL = false>
-__global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* __restrict__ h0,
+__global__ __launch_bounds__(512) void rnn_recur_mfma_kernel(const float* h0,
                                                              const float* __restrict__ Whh,
                                                              const float* __restrict__ b_ih,
                                                              const float* __restrict__ b_hh,
@@ -968,12 +964,8 @@ int rnn_step_launch(float* ht, const float* hp, const float* Whh, const float* b
     const size_t lds = sizeof(float) * ((size_t)(H + 4) * RS_COLS + 256 * RS_KS);
     if ((H % RS_COLS) != 0) return ASR_ERR_UNSUPPORTED;   // float4 column slices
     if (lds > 160 * 1024) return ASR_ERR_UNSUPPORTED;
-    static bool attr = false;
-    if (!attr) {
-        ASR_HIP_TRY(hipFuncSetAttribute((const void*)rnn_step_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    static AsrAttrOnce attr;
+    if (int r_ = attr.set((const void*)rnn_step_kernel, 160 * 1024)) return r_;
     const dim3 grid((unsigned)((H + RS_COLS - 1) / RS_COLS), (unsigned)((B + 31) / 32));
     hipLaunchKernelGGL(rnn_step_kernel, grid, dim3(256 * RS_KS), lds, s, ht, hp, Whh, b_ih, b_hh, B, H);
     ASR_LAUNCH_TRY();

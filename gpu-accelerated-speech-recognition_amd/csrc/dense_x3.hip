@@ -241,12 +241,8 @@ __global__ __launch_bounds__(64 * X3_WAVES) void gemm_x3_kernel(GemmArgs g, int 
 
 template <int NCH, int EPI>
 static int launch_gemm_x3_k(const GemmArgs& g, int tpw, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        ASR_HIP_TRY(hipFuncSetAttribute((const void*)gemm_x3_kernel<NCH, EPI>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, x3_gemm_lds<NCH>()));
-        attr = true;
-    }
+    static AsrAttrOnce attr;
+    if (int r_ = attr.set((const void*)gemm_x3_kernel<NCH, EPI>, x3_gemm_lds<NCH>())) return r_;
     const int ntile = (g.M + X3_ROWS - 1) / X3_ROWS;
     const int ncol = (g.N + X3_NCOL - 1) / X3_NCOL;
     int rows;
@@ -317,7 +313,7 @@ constexpr int x3_recur_lds() {
 }
 
 template <int NCH, bool EMIT, bool HL>
-__global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* __restrict__ h0,
+__global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
                                                                 const float* __restrict__ Whh,
                                                                 const float* __restrict__ b_ih,
                                                                 const float* __restrict__ b_hh, float* hid,
@@ -547,12 +543,8 @@ static int launch_recur_x3_k(const float* h0, const float* Whh, const float* b_i
                              float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int V,
                              float* hlast, hipStream_t s) {
     constexpr int lds = x3_recur_lds<NCH, EMIT>();
-    static bool attr = false;
-    if (!attr) {
-        ASR_HIP_TRY(hipFuncSetAttribute((const void*)rnn_recur_x3_kernel<NCH, EMIT, HL>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr = true;
-    }
+    static AsrAttrOnce attr;
+    if (int r_ = attr.set((const void*)rnn_recur_x3_kernel<NCH, EMIT, HL>, lds)) return r_;
     hipLaunchKernelGGL((rnn_recur_x3_kernel<NCH, EMIT, HL>), dim3((unsigned)((B + 15) / 16)), dim3(64 * NCH), lds,
                        s, h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast);
     ASR_LAUNCH_TRY();

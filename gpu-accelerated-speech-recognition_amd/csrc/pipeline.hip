@@ -100,6 +100,18 @@ struct asr_pipeline {
     long fail_from = -1;
     int fail_rc = ASR_OK;
     int hw_queues = 4, streams = 0;   // HIP hardware queues of the process, streams created
+    // every stream created: role (ASR_PIPE_ROLE_*) and CU range [lo, hi) of its mask
+    struct Placed { int role, lo, hi; hipStream_t s; };
+    std::vector<Placed> placed;
+    // Timeline (asr_pipeline_set_timing): per buffer, timing events at
+    // production start / end and decode start / end, read back per batch at
+    // its fetch as ms after the reference event ev_t0ref.
+    bool timing = false;
+    long timing_from = 0;
+    hipEvent_t ev_t0ref = nullptr;
+    std::vector<hipEvent_t> ev_t[4];
+    struct Stamp { long batch; float t[4]; };
+    std::vector<Stamp> timeline;
     // test hook (ASR_PIPELINE_FAULT=<batch>:<stage>, stage head|tail|produce|decode):
     // the named stage of that batch returns ASR_ERR_INTERNAL instead of queueing
     long fault_batch = -1;
@@ -129,6 +141,13 @@ int wave_occupancy(const asr_pipeline_config& c) {
 int auto_segments(const asr_pipeline_config& c, int kcap) {
     const bool x3s = asr::dense_x3_on() && kcap <= 64;
     return x3s && c.B >= 512 && c.B < 1024 ? 4 : (c.B < 512 || x3s) ? 2 : 1;
+}
+
+// Timeline stamp `which` (0 production start, 1 production end, 2 decode
+// start, 3 decode end) of buffer k on stream s, when timing is on.
+int mark(asr_pipeline* p, int which, int k, hipStream_t s) {
+    if (p->timing) ASR_HIP_TRY(hipEventRecord(p->ev_t[which][k], s));
+    return ASR_OK;
 }
 
 void set_failed(asr_pipeline* p, long from, int rc) {
@@ -163,6 +182,7 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     hipStream_t sp = p->s_prod[i % p->P];
     if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    if (int r = mark(p, 0, k, sp)) return r;
     asr_internal_rnn_kind = p->rnn_kind;
     asr_internal_graph_now = 1;
     int rc = asr_rnn_fwd(x, nullptr, p->W_ih, p->W_hh, p->b_ih, p->b_hh, p->hid[k], c.T, c.B, c.in, c.H, sp);
@@ -171,6 +191,7 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     if (!rc) rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
                                  ASR_EPI_BIAS_LOGSOFTMAX, sp);
     if (rc) return rc;
+    if (int r = mark(p, 1, k, sp)) return r;
     ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
     return ASR_OK;
 }
@@ -211,6 +232,7 @@ int produce_fused_segments(asr_pipeline* p, long i, const float* x, hipStream_t 
         if (rc) return rc;
         ASR_HIP_TRY(hipEventRecord(p->ev_seg[(size_t)k * p->S + s], sp));
     }
+    if (int r = mark(p, 1, k, sp)) return r;
     ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
     return ASR_OK;
 }
@@ -231,6 +253,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
     const long ga = std::min(p->grows, M);
     if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    if (int r = mark(p, 0, k, sp)) return r;
     if (p->S > 1) return produce_fused_segments(p, i, x, sp);
     int rc = ASR_OK;
     if (ga > 0) {
@@ -252,6 +275,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
     rc = asr_rnn_emit_fwd(nullptr, p->W_hh, p->b_ih, p->b_hh, p->W_out, p->b_out, p->hid[k], nullptr, p->emis[k],
                           c.T, c.B, c.H, c.V, sp);
     if (rc) return rc;
+    if (int r = mark(p, 1, k, sp)) return r;
     ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
     return ASR_OK;
 }
@@ -265,6 +289,7 @@ int produce_head(asr_pipeline* p, long i, const float* x) {
     // hid[k]'s previous batch: its emission GEMM has read it (stream order
     // when both GEMMs share s_gemm)
     if (p->tail_own) ASR_HIP_TRY(hipStreamWaitEvent(p->s_gemm, p->ev_ready[k], 0));
+    if (int r = mark(p, 0, k, p->s_gemm)) return r;
     asr_internal_gemm_tiled = p->gtiled;
     int rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], c.T * c.B, c.in, c.H, ASR_EPI_NONE, p->s_gemm);
     asr_internal_gemm_tiled = 0;
@@ -290,6 +315,7 @@ int produce_tail(asr_pipeline* p, long i) {
     int rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
                             ASR_EPI_BIAS_LOGSOFTMAX, p->s_tail);
     if (rc) return rc;
+    if (int r = mark(p, 1, k, p->s_tail)) return r;
     ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], p->s_tail));
     return ASR_OK;
 }
@@ -304,14 +330,17 @@ int enqueue_decode(asr_pipeline* p, long i) {
         for (int s = 0; s < p->S && !rc; s++) {
             const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
             ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_seg[(size_t)k * p->S + s], 0));
+            if (s == 0) if (int r = mark(p, 2, k, sd)) return r;
             rc = asr_ctc_decode_segment(p->dec[k], p->emis[k] + (long)t0 * c.B * c.V, c.T, t0, t1, c.B,
                                         (long)c.B * c.V, c.V, nullptr, 1, sd);
         }
     } else {
         ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_ready[k], 0));
+        if (int r = mark(p, 2, k, sd)) return r;
         rc = asr_ctc_decode(p->dec[k], p->emis[k], c.T, c.B, 1, sd);
     }
     if (rc) return rc;
+    if (int r = mark(p, 3, k, sd)) return r;
     ASR_HIP_TRY(hipEventRecord(p->ev_free[k], sd));
     p->decoded = i + 1;
     return ASR_OK;
@@ -328,6 +357,7 @@ int produce_group_head(asr_pipeline* p, long i, const float* x) {
     if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     hipStream_t sp = p->s_prod[(i / p->G) % p->P];
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
+    if (int r = mark(p, 0, k, sp)) return r;
     return asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], c.T * c.B, c.in, c.H, ASR_EPI_NONE, sp);
 }
 
@@ -348,6 +378,7 @@ int flush_group(asr_pipeline* p) {
         const int k = (int)(g[j] % p->nbuf);
         rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
                             ASR_EPI_BIAS_LOGSOFTMAX, sp);
+        if (!rc) rc = mark(p, 1, k, sp);
         if (!rc && hipEventRecord(p->ev_ready[k], sp) != hipSuccess) rc = ASR_ERR_HIP;
         if (!rc) rc = enqueue_decode(p, g[j]);
     }
@@ -394,15 +425,25 @@ int fetch_to(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, do
     const bool drain_tail = p->pending_tail >= 0 && j + p->D >= p->pending_tail;
     const bool drain_group = !p->group.empty() && j + p->D >= p->group.front();
     if (j >= p->decoded || drain_tail || drain_group) {
+        // a failed flush fails the pipeline from the flushed batch on
+        // (set_failed); batch j itself is returned normally when it was
+        // already decoded (the header's promise for earlier batches)
         int rc = flush_tail(p);
         if (!rc) rc = flush_group(p);
-        if (rc) return rc;
+        if (rc && (j >= p->decoded || (p->fail_from >= 0 && j >= p->fail_from))) return rc;
     }
     if (j >= p->decoded) return ASR_ERR_INTERNAL;   // never queued (cannot happen once flushed)
     asr_ctc_t* h = p->dec[j % p->nbuf];
     *res_rc = asr_ctc_get_best(h, labels, max_len, lengths, logp);
     if (*res_rc != ASR_OK && *res_rc != ASR_ERR_BEAM_OVERFLOW) return *res_rc;
     if (ms) asr_ctc_last_kernel_ms(h, ms);
+    if (p->timing && j >= p->timing_from) {   // the batch's stamps, all complete once its decode is
+        const int k = (int)(j % p->nbuf);
+        ASR_HIP_TRY(hipEventSynchronize(p->ev_t[3][k]));
+        asr_pipeline::Stamp st{j, {0.f, 0.f, 0.f, 0.f}};
+        for (int w = 0; w < 4; w++) ASR_HIP_TRY(hipEventElapsedTime(&st.t[w], p->ev_t0ref, p->ev_t[w][k]));
+        p->timeline.push_back(st);
+    }
     *batch = j;
     p->collected = j + 1;
     return ASR_OK;
@@ -429,8 +470,10 @@ void release(asr_pipeline* p) {
     for (auto b : p->emis) hipFree(b);
     for (auto b : p->hst) hipFree(b);
     for (auto e : p->ev_seg) if (e) hipEventDestroy(e);
-    for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec})
+    for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec, &p->ev_t[0], &p->ev_t[1], &p->ev_t[2],
+                    &p->ev_t[3]})
         for (auto e : *v) if (e) hipEventDestroy(e);
+    if (p->ev_t0ref) hipEventDestroy(p->ev_t0ref);
     for (auto s : p->s_dec) if (s) hipStreamDestroy(s);
     for (auto s : p->s_prod) if (s) hipStreamDestroy(s);
     if (p->s_gemm) hipStreamDestroy(p->s_gemm);
@@ -438,9 +481,71 @@ void release(asr_pipeline* p) {
     if (p->s_gdec) hipStreamDestroy(p->s_gdec);
 }
 
+// Placement probe: every workgroup records the XCD (HW_REG_XCC_ID) and the
+// shader engine / array / CU (HW_REG_HW_ID bits 15:8) its wave runs on, after
+// a short spin so that the grid spreads over every CU the stream's mask
+// allows.  Reads two hardware registers; nothing else.
+constexpr int PROBE_BLOCKS = 8192;
+__global__ __launch_bounds__(64) void placement_probe_kernel(uint32_t* out, long long spin) {
+    // s_getreg immediates: id | offset << 6 | (size - 1) << 11
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11));   // HW_REG_XCC_ID
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));     // HW_REG_HW_ID
+    const long long t0 = clock64();
+    while (clock64() - t0 < spin) __builtin_amdgcn_s_sleep(1);
+    if (threadIdx.x == 0) out[blockIdx.x] = ((xcc & 0xFu) << 16) | ((hw >> 8) & 0xFFu);
+}
+
 }  // namespace
 
 extern "C" {
+
+int asr_pipeline_get_placement(asr_pipeline_t* p, int cap, int* n, int* role, int* cu_lo, int* cu_hi) {
+    if (!p || !n || cap < 0 || (cap > 0 && (!role || !cu_lo || !cu_hi))) return ASR_ERR_ARG;
+    *n = (int)p->placed.size();
+    for (int i = 0; i < std::min(cap, *n); i++) {
+        role[i] = p->placed[i].role;
+        cu_lo[i] = p->placed[i].lo;
+        cu_hi[i] = p->placed[i].hi;
+    }
+    return ASR_OK;
+}
+
+int asr_pipeline_probe_placement(asr_pipeline_t* p, int role, int* cus_per_xcc, int* n_xcc) {
+    if (!p || !cus_per_xcc || !n_xcc) return ASR_ERR_ARG;
+    hipStream_t st = nullptr;
+    for (const auto& q : p->placed)
+        if (q.role == role) { st = q.s; break; }
+    if (!st) return ASR_ERR_ARG;
+    for (int x = 0; x < ASR_MAX_XCC; x++) cus_per_xcc[x] = 0;
+    *n_xcc = 0;
+    uint32_t* d = nullptr;
+    ASR_HIP_TRY(hipMalloc(&d, sizeof(uint32_t) * PROBE_BLOCKS));
+    std::vector<uint32_t> h(PROBE_BLOCKS, 0xFFFFFFFFu);
+    int rc = ASR_OK;
+    if (hipMemsetAsync(d, 0xFF, sizeof(uint32_t) * PROBE_BLOCKS, st) != hipSuccess) rc = ASR_ERR_HIP;
+    if (!rc) {
+        hipLaunchKernelGGL(placement_probe_kernel, dim3(PROBE_BLOCKS), dim3(64), 0, st, d, 20000ll);
+        if (hipGetLastError() != hipSuccess) rc = ASR_ERR_HIP;
+    }
+    if (!rc && hipMemcpyAsync(h.data(), d, sizeof(uint32_t) * PROBE_BLOCKS, hipMemcpyDeviceToHost, st) != hipSuccess)
+        rc = ASR_ERR_HIP;
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = ASR_ERR_HIP;
+    hipFree(d);
+    if (rc) return rc;
+    std::vector<char> seen((size_t)ASR_MAX_XCC * 256, 0);
+    for (uint32_t v : h) {
+        if (v == 0xFFFFFFFFu) return ASR_ERR_INTERNAL;   // a workgroup never wrote
+        const uint32_t x = (v >> 16) & 0xFu, cu = v & 0xFFu;
+        if (x >= (uint32_t)ASR_MAX_XCC) return ASR_ERR_INTERNAL;
+        char& s = seen[(size_t)x * 256 + cu];
+        if (!s) {
+            s = 1;
+            cus_per_xcc[x]++;
+            *n_xcc = std::max(*n_xcc, (int)x + 1);
+        }
+    }
+    return ASR_OK;
+}
 
 int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const float* W_hh,
                         const float* b_ih, const float* b_hh, const float* W_out, const float* b_out,
@@ -573,7 +678,6 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->G = (c.H > 256 && (c.H % 128) == 0 && (c.B % 16) == 0) ? std::max(1, std::min(4, Gw)) : 1;
         p->D = c.inflight ? c.inflight : std::max(1, std::min(2 * p->G, ncu / bcu - 1));
         p->P = c.prod_streams ? c.prod_streams : (c.H > 256 ? 2 : 1);
-        if (p->D == 1) p->gcu = 0;
     } else {   // chip-filling batches otherwise (C3's beam 100, BL's H = 2048): one decode at a time
         p->mode = SHARED;
         p->dcus = c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : 0;
@@ -588,13 +692,6 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
             p->fuse = c.V <= 32;
         }
     }
-    // CU groups (GROUPS / GROUPS2): decode d runs on group d % ngroups, so an
-    // explicit inflight beyond the groups queues decodes behind a group's
-    // current one.  Not the default: one or two queued decodes measured
-    // slower here (C2 50.8 -> 42.5 / 47.4 M frames/s, C5 3.37 -> 1.54 /
-    // 1.39 M; profiles/r04/bench_scan.md), unlike the chip-filling mode.
-    if (p->mode != SHARED && p->gcu) p->ngroups = std::max(1, std::min(p->D, ncu / p->gcu - 1));
-    if (p->mode != SHARED && p->D > 1 && (p->ngroups + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
     // T-segments (fused production only): explicit (config.segments), else 2 for small shards (under 512 utterances: the job's fill
     // and drain are a large part of it; measured at 256 per GPU, 20 steps:
     // 1 / 2 / 4 segments 132.5 / 136.4 / 134.7 M frames/s), 1 otherwise
@@ -628,28 +725,43 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->tail_own = p->split && nstreams() < p->hw_queues;
         p->streams = nstreams() + (p->tail_own ? 1 : 0);
     }
+    // CU groups (GROUPS / GROUPS2), from the decode count the queue fit left:
+    // decode d runs on group d % ngroups, so an explicit inflight beyond the
+    // groups queues decodes behind a group's current one.  Not the default:
+    // one or two queued decodes measured slower here (C2 50.8 -> 42.5 / 47.4 M
+    // frames/s, C5 3.37 -> 1.54 / 1.39 M; profiles/r04/bench_scan.md), unlike
+    // the chip-filling mode.  One decode in flight (GROUPS2) runs on every CU.
+    if (p->mode == GROUPS2 && p->D == 1) p->gcu = 0;
+    if (p->mode != SHARED && p->gcu) p->ngroups = std::max(1, std::min(p->D, ncu / p->gcu - 1));
+    if (p->mode != SHARED && p->D > 1 && (p->ngroups + 1) * p->gcu > ncu) { delete p; return ASR_ERR_UNSUPPORTED; }
     // D decoding + P producing (+1: split production queues the next input
     // projection before the previous batch's emission projection)
     p->nbuf = p->D + p->P + (p->split ? 1 : 0);
     if (p->G > 1) p->nbuf = p->D + (p->P + 1) * p->G;   // P groups producing, one filling, D decoding
     if (p->nbuf < 2) p->nbuf = 2;
     // streams
-    auto mk = [&](hipStream_t* s, int lo, int hi) { return rc ? rc : (rc = cu_stream(s, ncu, lo, hi)); };
+    auto mkr = [&](int role, hipStream_t* s, int lo, int hi) {
+        if (rc) return rc;
+        rc = cu_stream(s, ncu, lo, hi);
+        if (!rc) p->placed.push_back({role, std::max(0, lo), std::min(ncu, hi), *s});
+        return rc;
+    };
     p->s_dec.assign(p->D, nullptr);
     p->s_prod.assign(p->P, nullptr);
     if (p->mode == SHARED) {
         // every decode on all of the decode CUs (decode d on its own 1/D of
         // them, several rounds of utterances per CU: 206.7 -> 196.9 M frames/s
         // at C4, D = 2, profiles/r04/bench_scan.md)
-        for (int d = 0; d < p->D; d++) mk(&p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
-        for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->dcus, ncu);
-        if (p->grows > 0) mk(&p->s_gdec, 0, p->dcus);
+        for (int d = 0; d < p->D; d++) mkr(ASR_PIPE_ROLE_DECODE, &p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
+        for (int q = 0; q < p->P; q++) mkr(ASR_PIPE_ROLE_PRODUCTION, &p->s_prod[q], p->dcus, ncu);
+        if (p->grows > 0) mkr(ASR_PIPE_ROLE_DECODE_CU_GEMM, &p->s_gdec, 0, p->dcus);
     } else {
         for (int d = 0; d < p->D; d++)
-            mk(&p->s_dec[d], p->gcu ? (d % p->ngroups) * p->gcu : 0, p->gcu ? (d % p->ngroups + 1) * p->gcu : ncu);
-        for (int q = 0; q < p->P; q++) mk(&p->s_prod[q], p->gcu ? p->ngroups * p->gcu : 0, ncu);
-        if (p->split) mk(&p->s_gemm, 0, ncu);   // the GEMMs on every CU
-        if (p->tail_own) mk(&p->s_tail, 0, ncu);
+            mkr(ASR_PIPE_ROLE_DECODE, &p->s_dec[d], p->gcu ? (d % p->ngroups) * p->gcu : 0,
+                p->gcu ? (d % p->ngroups + 1) * p->gcu : ncu);
+        for (int q = 0; q < p->P; q++) mkr(ASR_PIPE_ROLE_PRODUCTION, &p->s_prod[q], p->gcu ? p->ngroups * p->gcu : 0, ncu);
+        if (p->split) mkr(ASR_PIPE_ROLE_GEMM, &p->s_gemm, 0, ncu);   // the GEMMs on every CU
+        if (p->tail_own) mkr(ASR_PIPE_ROLE_GEMM, &p->s_tail, 0, ncu);
         else p->s_tail = p->s_gemm;
     }
     // buffers, decoders, events
@@ -836,6 +948,36 @@ int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues) {
     if (!p) return ASR_ERR_ARG;
     if (streams) *streams = p->streams;
     if (hw_queues) *hw_queues = p->hw_queues;
+    return ASR_OK;
+}
+
+int asr_pipeline_set_timing(asr_pipeline_t* p, int on) {
+    if (!p) return ASR_ERR_ARG;
+    if (on && p->ev_t[0].empty()) {
+        for (int w = 0; w < 4; w++) {
+            p->ev_t[w].assign(p->nbuf, nullptr);
+            for (auto& e : p->ev_t[w]) ASR_HIP_TRY(hipEventCreate(&e));
+        }
+        ASR_HIP_TRY(hipEventCreate(&p->ev_t0ref));
+    }
+    p->timeline.clear();
+    p->timing = on != 0;
+    p->timing_from = p->submitted;
+    if (on) {   // the reference: now, on an idle device (the caller drained the pipeline)
+        ASR_HIP_TRY(hipDeviceSynchronize());
+        ASR_HIP_TRY(hipEventRecord(p->ev_t0ref, p->s_dec[0]));
+        ASR_HIP_TRY(hipEventSynchronize(p->ev_t0ref));
+    }
+    return ASR_OK;
+}
+
+int asr_pipeline_get_timeline(asr_pipeline_t* p, int cap, int* n, long long* batch, float* t) {
+    if (!p || !n || cap < 0 || (cap > 0 && (!batch || !t))) return ASR_ERR_ARG;
+    *n = (int)p->timeline.size();
+    for (int i = 0; i < std::min(cap, *n); i++) {
+        batch[i] = p->timeline[i].batch;
+        for (int w = 0; w < 4; w++) t[4 * i + w] = p->timeline[i].t[w];
+    }
     return ASR_OK;
 }
 

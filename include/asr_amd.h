@@ -403,12 +403,39 @@ int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode
  * hw_queues only when the caller fixed inflight / prod_streams.  DESIGN.md
  * §7c gives the measured cost. */
 int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues);
+/* Where the pipeline's streams run: for each stream it created, its role
+ * (ASR_PIPE_ROLE_*) and the CU range [cu_lo, cu_hi) of its CU mask
+ * (hipExtStreamCreateWithCUMask bits; [0, ncu) = unmasked).  *n = streams
+ * created; the first min(cap, *n) entries are written. */
+enum { ASR_PIPE_ROLE_DECODE = 0, ASR_PIPE_ROLE_PRODUCTION = 1, ASR_PIPE_ROLE_DECODE_CU_GEMM = 2,
+       ASR_PIPE_ROLE_GEMM = 3 };
+#define ASR_MAX_XCC 16
+int asr_pipeline_get_placement(asr_pipeline_t* p, int cap, int* n, int* role, int* cu_lo, int* cu_hi);
+/* Diagnostic: the physical CUs the first stream of `role` reaches, counted per
+ * XCD (cus_per_xcc[ASR_MAX_XCC], *n_xcc = XCDs seen): one probe launch of
+ * 8192 short workgroups on that stream that read HW_REG_XCC_ID / HW_REG_HW_ID
+ * (synchronises the stream).  Workgroups are dealt round-robin over the XCDs
+ * whatever the mask, so a role runs evenly only when its mask holds the same
+ * number of CUs in every XCD; DESIGN.md §7f. */
+int asr_pipeline_probe_placement(asr_pipeline_t* p, int role, int* cus_per_xcc, int* n_xcc);
 /* The emissions [T][B][V] (log-probabilities, device) that the decode of the
  * batch last returned by asr_pipeline_collect consumed — the exact bytes, for
  * parity checks of the pipelined path.  Valid until the next submit that
  * reuses the buffer; ASR_ERR_STATE if nothing was collected yet or the
  * buffer has been reused. */
 int asr_pipeline_peek_emissions(asr_pipeline_t* p, const float** d_emis);
+/* Timeline (measurement): with timing on, every batch submitted from now on
+ * records four timing events — its production's start and end on the
+ * production stream(s) and its decode's start (the first decode kernel
+ * queued behind its emissions) and end on its decode stream — read back when
+ * the batch is collected, as ms after the moment of this call.  Call it on
+ * a drained pipeline (it synchronises the device); it clears the timeline.
+ * A decode's "start" is when its stream reached it, which may be before
+ * its workgroups get CUs.  asr_pipeline_get_timeline: *n = batches recorded;
+ * the first min(cap, *n) as batch[i] and t[i][4] = (production start,
+ * production end, decode start, decode end). */
+int asr_pipeline_set_timing(asr_pipeline_t* p, int on);
+int asr_pipeline_get_timeline(asr_pipeline_t* p, int cap, int* n, long long* batch, float* t);
 int asr_pipeline_destroy(asr_pipeline_t* p);
 
 #ifdef __cplusplus

@@ -129,3 +129,25 @@ def test_segment_errors():
         d.decode_segment(ew.ptr, T, 0, 10, B, False)
     assert e.value.status == asr.ASR_ERR_UNSUPPORTED
     d.close()
+
+
+def test_segmented_overflow_retry_equals_whole():
+    """a segmented decode whose beam overflows the automatic
+    capacity (flat emissions: more tied survivors than max_states) is
+    re-decoded whole at the results fetch, from the first segment's
+    emission pointer and lengths; the result is the oracle's and the
+    whole decode's, bit for bit."""
+    T, B, V, beam = 8, 3, 4, 3
+    uni = np.full((T, B, V), 1.0 / V, np.float32)
+    ref = oracle.decode(uni, beam, 0, max_hyps=4096)
+    d_em = asr.DeviceMatrix.from_numpy(uni.reshape(T * B, V))
+    d = asr.CTCDecoder(V, beam, 0)
+    assert d.config()[0] < max(len(r) for r in ref)   # the default capacity overflows
+    for t0, t1 in ((0, 3), (3, 5), (5, T)):
+        d.decode_segment(d_em.ptr + 4 * t0 * B * V, T, t0, t1, B, False)
+    lab, lp = d.best()
+    assert lab == [r[0][0] for r in ref]
+    assert_beams_equal(d.beams(max_hyps=4096), ref, "segmented overflow retry")
+    d.close()
+    whole = _whole(d_em, T, B, V, beam, False, waves=0)
+    assert lab == whole[1] and np.array_equal(lp, whole[2])

@@ -275,6 +275,95 @@ def test_pipeline_fits_hw_queues(monkeypatch):
     assert dq["inflight"] == 3 and dq["prod_streams"] == 3 and dq["streams"] > 4, dq
 
 
+def _covers(pl, ncu):
+    """Every CU is in a decode range or the production range, and no decode
+    range overlaps the production range."""
+    rs = pl.placement()
+    dec = [(lo, hi) for r, lo, hi in rs if r == "decode"]
+    prod = [(lo, hi) for r, lo, hi in rs if r == "production"]
+    assert dec and prod, rs
+    cov = np.zeros(ncu, bool)
+    for lo, hi in dec + prod:
+        cov[lo:hi] = True
+    assert cov.all(), (rs, np.flatnonzero(~cov))
+    for dlo, dhi in dec:
+        for plo, phi in prod:
+            if (dlo, dhi) != (0, ncu) and (plo, phi) != (0, ncu):
+                assert dhi <= plo or phi <= dlo, rs
+    return rs
+
+
+@pytest.mark.parametrize("T,B,inp,H,V,beam,mode", [
+    (24, 64, 64, 256, 29, 50, "CU groups (small batches)"),
+    (16, 32, 32, 384, 29, 8, "CU groups (H > 256)"),
+])
+def test_pipeline_groups_fit_hw_queues(monkeypatch, T, B, inp, H, V, beam, mode):
+    """the CU groups are laid out from the decode count that the
+    hardware-queue fit leaves (at HIP's default of 4 queues the small-batch
+    schedule drops from 3 decodes to 2): every CU is then in a decode group
+    or in production, never in neither, and the results are the sequential
+    ones."""
+    import torch
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    W = _weights(inp, H, V, seed=B + H)
+    x = asr.DeviceMatrix.from_numpy(np.random.default_rng(5).uniform(-1, 1, (T * B, inp)).astype(np.float32))
+    full = asr.Pipeline(T, B, inp, H, V, beam, W)
+    assert full.describe()["mode"] == mode
+    _covers(full, ncu)
+    full.close()
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert d["hw_queues"] == 4 and d["streams"] <= 4, d
+    rs = _covers(p, ncu)
+    ndec = len({(lo, hi) for r, lo, hi in rs if r == "decode"})
+    assert ndec == min(d["inflight"], len([r for r in rs if r[0] == "decode"])), (rs, d)
+    for _ in range(3):
+        p.submit(x)
+    got = []
+    while p.pending():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    p.close()
+    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_AUTO)
+    for g in got:
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+
+
+def test_pipeline_timeline_and_probe():
+    """asr_pipeline_set_timing / get_timeline: one record per batch collected
+    after the call, stamps ordered within each stage; the results are those
+    of an untimed run.  asr_pipeline_probe_placement: the decode and
+    production roles reach CUs on every XCD, at most their ranges' CUs."""
+    T, B, inp, H, V, beam = 24, 600, 64, 256, 29, 30
+    W = _weights(inp, H, V, seed=21)
+    x = asr.DeviceMatrix.from_numpy(np.random.default_rng(3).uniform(-1, 1, (T * B, inp)).astype(np.float32))
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    p.submit(x)
+    p.collect()
+    p.set_timing(True)
+    n = 5
+    got = []
+    for _ in range(n):
+        p.submit(x)
+    while p.pending():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    bid, st = p.timeline()
+    assert list(bid) == list(range(1, 1 + n)), bid
+    assert (st >= 0).all() and (st[:, 1] >= st[:, 0]).all() and (st[:, 3] >= st[:, 2]).all(), st
+    assert (st[:, 3] >= st[:, 0]).all(), st
+    ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
+    for g in got:
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+    rs = p.placement()
+    for role in ("decode", "production"):
+        lo, hi = next((lo, hi) for r, lo, hi in rs if r == role)
+        per = p.probe_placement(role)
+        assert len(per) >= 1 and all(c > 0 for c in per) and sum(per) <= hi - lo, (role, per, lo, hi)
+    p.close()
+
+
 def test_pipeline_latches_dense_arith():
     """A pipeline keeps the dense arithmetic it was created under
     (asr_set_dense_arith changes the process-wide setting for later calls
