@@ -47,6 +47,21 @@ int dense_arith() {
 void dense_arith_set(int a) { g_dense_arith.store(a, std::memory_order_relaxed); }
 bool dense_x3_on() { return dense_arith() == ASR_DENSE_SPLIT_BF16; }
 
+// A/B build knobs (Makefile dvariant; measured with tools/dense_time.py, run sa:
+// only the GEMM prefetch is on in the product; the others changed < 1 %)
+#ifndef ASR_X3G_PF
+#define ASR_X3G_PF 1     // GEMM: A fragments one chunk ahead (C4 input projection 1.345 -> 1.230 ms on 128 CUs)
+#endif
+#ifndef ASR_X3G_SGB
+#define ASR_X3G_SGB 0    // GEMM: sched_group_barrier order of reads / MFMAs
+#endif
+#ifndef ASR_X3R_TANH
+#define ASR_X3R_TANH 0   // recurrence: branch-free exp2 / rcp tanh (<= 1.6 ulp)
+#endif
+#ifndef ASR_X3R_PACK
+#define ASR_X3R_PACK 0   // recurrence: k order permuted in each 32-chunk, h pieces written as bf16 pairs
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -56,6 +71,51 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
     const float r = x - (float)h;
     m = (__bf16)r;
     l = (__bf16)(r - (float)m);
+}
+
+__device__ __forceinline__ float fbits(unsigned u) { return __builtin_bit_cast(float, u); }
+
+// tanh of the recurrence epilogue.  ASR_X3R_TANH: branch-free, |x| >= 0.625
+// as 1 - 2 / (1 + 2^(2|x| log2 e)) (v_exp_f32, v_rcp_f32), below an odd
+// minimax polynomial; <= 1.6 ulp from tanhf over every fp32 input
+// (tools/x3_probe.hip tanh_fast); else the device library's tanhf.
+__device__ __forceinline__ float x3_tanh(float x) {
+#if ASR_X3R_TANH
+    const float ax = fabsf(x);
+    const float y = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);
+    const float big = __builtin_fmaf(__builtin_amdgcn_rcpf(1.0f + y), -2.0f, 1.0f);
+    const float x2 = x * x;
+    float q = __builtin_fmaf(fbits(0xbbbac73du), x2, fbits(0x3ca908c9u));
+    q = __builtin_fmaf(x2, q, fbits(0xbd5c1c4eu));
+    q = __builtin_fmaf(x2, q, fbits(0x3e088382u));
+    q = __builtin_fmaf(x2, q, fbits(0xbeaaaa99u));
+    const float small = __builtin_fmaf(x2, ax * q, ax);
+    const float m = ax < 0.625f ? small : big;
+    return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, m) & 0x7fffffffu) |
+                                         (__builtin_bit_cast(unsigned, x) & 0x80000000u));
+#else
+    return tanhf(x);
+#endif
+}
+
+// Position of h column n in the LDS piece rows (and of k in a 32-deep MFMA
+// chunk): ASR_X3R_PACK puts columns n and n + 16 of a 32-column slice side by
+// side, so the lane that produces both writes one bf16 pair per piece.  The
+// B / W_out fragments follow the same k order (x3_kperm).
+__device__ __forceinline__ int x3_hpos(int n) {
+#if ASR_X3R_PACK
+    return (n & ~31) + 2 * (n & 15) + ((n >> 4) & 1);
+#else
+    return n;
+#endif
+}
+// k of element j of lane group g in chunk c (A / B fragment element order)
+__device__ __forceinline__ int x3_kperm(int c, int g, int j) {
+#if ASR_X3R_PACK
+    return 32 * c + 16 * (j & 1) + 4 * g + (j >> 1);
+#else
+    return 32 * c + 8 * g + j;
+#endif
 }
 
 // raw buffer resources: loads past num_records return 0, stores are dropped
@@ -210,6 +270,29 @@ __global__ __launch_bounds__(64 * X3_WAVES) void gemm_x3_kernel(GemmArgs g, int 
     for (; tile < tend; tile += tstep) {
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
         const __bf16* pb = x3s + cur * 3 * PIECE;
+#if ASR_X3G_PF
+        // A fragments one chunk ahead (two register sets), so that a chunk's
+        // MFMAs never wait on its own LDS reads
+        {
+            bf16x8 fa[2][3];
+            auto rd = [&](int c, int sl) {
+                const int off = c15 * AS + 32 * c + 8 * gq;
+                fa[sl][0] = *reinterpret_cast<const bf16x8*>(pb + off);
+                fa[sl][1] = *reinterpret_cast<const bf16x8*>(pb + PIECE + off);
+                fa[sl][2] = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
+            };
+            rd(0, 0);
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                if (c + 1 < NCH) rd(c + 1, (c + 1) & 1);
+                X3_PRODUCTS(2, acc, fa[c & 1][0], fa[c & 1][1], fa[c & 1][2], bh, bm, bl, c)
+#if ASR_X3G_SGB
+                if (c + 1 < NCH) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+#endif
+            }
+        }
+#else
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int off = c15 * AS + 32 * c + 8 * gq;
@@ -218,6 +301,7 @@ __global__ __launch_bounds__(64 * X3_WAVES) void gemm_x3_kernel(GemmArgs g, int 
             const bf16x8 al = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
             X3_PRODUCTS(2, acc, ah, am, al, bh, bm, bl, c)
         }
+#endif
         stage(cur ^ 1);
         load(tile + 2 * tstep);
         const long r0 = (long)tile * X3_ROWS;
@@ -345,7 +429,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 __bf16 h, m, l;
-                split3(Whh[(long)(32 * c + 8 * gq + j) * H + n], h, m, l);
+                split3(Whh[(long)x3_kperm(c, gq, j) * H + n], h, m, l);
                 bh[ct][c][j] = h;
                 bm[ct][c][j] = m;
                 bl[ct][c][j] = l;
@@ -357,9 +441,10 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
         const float v = (h0 && r0 + r < B) ? h0[(long)(r0 + r) * H + k] : 0.f;
         __bf16 a, b, c;
         split3(v, a, b, c);
-        hsb[r * AS + k] = a;
-        hsb[PIECE + r * AS + k] = b;
-        hsb[2 * PIECE + r * AS + k] = c;
+        const int o = r * AS + x3_hpos(k);
+        hsb[o] = a;
+        hsb[PIECE + o] = b;
+        hsb[2 * PIECE + o] = c;
     }
     float bo0 = 0.f, bo1 = 0.f;
     if (EMIT) {
@@ -371,7 +456,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
             bf16x8 fh, fm, fl;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const int k = 32 * c + 8 * (l >> 4) + j;
+                const int k = x3_kperm(c, l >> 4, j);
                 __bf16 a, b, cc;
                 split3(col < V ? Wout[(long)k * V + col] : 0.f, a, b, cc);
                 fh[j] = a;
@@ -493,11 +578,29 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
         }
         __bf16* hn = hsb + (cur ^ 1) * 3 * PIECE;
         const auto rs = brsrc(hdst + t * tstride, (!EMIT || hdst) ? slab : 0);
+#if ASR_X3R_PACK
+        // columns n and n + 16 are adjacent in the piece rows: one bf16 pair per piece and row
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            __bf16 a[2], b[2], c[2];
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const float h = x3_tanh((p[ct][j] + acc[ct][j]) + bias[ct]);
+                split3(h, a[ct], b[ct], c[ct]);
+                bstore(rs, voff[ct] + j * H * 4, h);
+            }
+            const int o = (4 * gq + j) * AS + 32 * w + 2 * c15;
+            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<bf16x2*>(hn + o) = bf16x2{a[0], a[1]};
+            *reinterpret_cast<bf16x2*>(hn + PIECE + o) = bf16x2{b[0], b[1]};
+            *reinterpret_cast<bf16x2*>(hn + 2 * PIECE + o) = bf16x2{c[0], c[1]};
+        }
+#else
 #pragma unroll
         for (int ct = 0; ct < 2; ct++) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const float h = tanhf((p[ct][j] + acc[ct][j]) + bias[ct]);
+                const float h = x3_tanh((p[ct][j] + acc[ct][j]) + bias[ct]);
                 __bf16 a, b, c;
                 split3(h, a, b, c);
                 const int o = (4 * gq + j) * AS + ncol[ct];
@@ -507,6 +610,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
                 bstore(rs, voff[ct] + j * H * 4, h);
             }
         }
+#endif
         if (EMIT) {
             // after h_t (acc, P_t dead: fewer live registers): h_{t-1}'s
             // partial (h_{t-1} is in buffer cur, not overwritten before the
@@ -524,7 +628,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
     if (HL && hlast) {
         for (int x = tid; x < 16 * H; x += 64 * NW) {
             const int r = x / H, k = x - r * H;
-            const int o = r * AS + k;
+            const int o = r * AS + x3_hpos(k);
             if (r0 + r < B) hlast[(long)(r0 + r) * H + k] = ((float)pl[o] + (float)pl[PIECE + o]) + (float)pl[2 * PIECE + o];
         }
     }

@@ -55,6 +55,10 @@ def main():
                          "GEMM whose full-size standalone run has the most MFMAs)")
     ap.add_argument("--slice", action="append", default=[],
                     help="kernel=CUs of that kernel's smaller dispatch groups (overrides --slice-cus)")
+    ap.add_argument("--wpw", action="append", default=[],
+                    help="kernel=waves per workgroup: a dispatch group's busy CUs are then "
+                         "min(its mask's CUs, SQ_WAVES / wpw), the kernels running one workgroup per CU "
+                         "(default 8 for gemm_x3_kernel / rnn_recur_x3_kernel / rnn_recur_mfma_kernel)")
     ap.add_argument("--T", type=int, required=True)
     ap.add_argument("--B", type=int, required=True)
     ap.add_argument("--decoder", default="ctc_wave_kernel")
@@ -63,6 +67,8 @@ def main():
     ap.add_argument("--round", default="r04")
     args = ap.parse_args()
     cus = dict(x.split("=") for x in args.cus)
+    wpw = {"gemm_x3_kernel": 8, "rnn_recur_x3_kernel": 8, "rnn_recur_mfma_kernel": 8}
+    wpw.update({k: int(v) for k, v in (x.split("=") for x in args.wpw)})
     per, meta = load(args.mfma)
     groups = collections.defaultdict(list)
     for d, c in per.items():
@@ -82,9 +88,17 @@ def main():
             ncu = sl or ncu
         avg = {k: sum(c[k] for c, _ in lst) / len(lst) for k in lst[0][0]}
         secs = sum(s for _, s in lst) / len(lst)
+        # one workgroup per CU: the group's own workgroup count bounds its busy CUs
+        # (a 1024-utterance recurrence is 64 workgroups on a 128-CU mask)
+        cus_src = "CU mask"
+        w = next((v for k, v in wpw.items() if k in name), None)
+        if w and avg.get("SQ_WAVES"):
+            nwg = int(round(avg["SQ_WAVES"] / w))
+            if nwg < ncu:
+                ncu, cus_src = nwg, f"SQ_WAVES / {w} waves per workgroup"
         wall = avg["GRBM_GUI_ACTIVE"] / 8.0
         bf16 = 512.0 * avg.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) / 1e9
-        rec = {"dispatches": len(lst), "cus": ncu, "mfma_f32_insts": round(avg["SQ_INSTS_VALU_MFMA_F32"]),
+        rec = {"dispatches": len(lst), "cus": ncu, "cus_source": cus_src, "mfma_f32_insts": round(avg["SQ_INSTS_VALU_MFMA_F32"]),
                "mfma_bf16_insts": round(avg.get("SQ_INSTS_VALU_MFMA_BF16", 0.0)),
                "gflop": round(512.0 * avg["SQ_INSTS_VALU_MFMA_MOPS_F32"] / 1e9 + bf16 / 6.0, 2),
                "bf16_gflop": round(bf16, 2),
