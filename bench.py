@@ -405,6 +405,39 @@ class ClockSampler:
                 "hotspot_c_max": round(float(max(tp)), 1) if tp else None}
 
 
+def serialized_decode(asr, em_host, T, Bp, V, beam, dcus, conc, reps=2):
+    """The decoder alone, live, after the timed region: `conc` decodes of the
+    last batch's emissions at once, one per stream over the pipeline's decode
+    CUs [0, dcus) (the decodes the pipeline keeps resident there: 16
+    utterances per CU), with the pipeline's decoder schedule; HIP events on
+    those streams.  Returns ms per decode launch (the max over the streams of
+    a round, divided by conc) — the kernel's own time at the pipeline's load,
+    without the queue wait the timed region's event spans include."""
+    d_em = asr.DeviceMatrix.from_numpy(np.ascontiguousarray(em_host).reshape(T * Bp, V))
+    sts = [cu_range_stream(0, dcus) for _ in range(conc)]
+    decs = [asr.CTCDecoder(V, beam, 0, waves=asr.ASR_CTC_WAVES_LIST) for _ in range(conc)]
+    for d in decs:
+        d.set_concurrency(conc)
+    best = None
+    for _ in range(reps + 1):   # the first round sizes the workspaces
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(sts[0])
+        ends = []
+        for st, d in zip(sts, decs):
+            st.wait_event(e0)
+            d.decode_device(d_em.ptr, T, Bp, is_log=True, stream=st.cuda_stream)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(st)
+            ends.append(e1)
+        for e in ends:
+            e.synchronize()
+        ms = max(e0.elapsed_time(e) for e in ends)
+        best = ms if best is None else min(best, ms)
+    for d in decs:
+        d.close()
+    return best / conc
+
+
 def union_ms(iv):
     """Total length of the union of intervals [(a, b)]."""
     tot, end = 0.0, None
@@ -509,6 +542,9 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--decode-only", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-serialized", action="store_true",
+                    help="skip the live stand-alone decoder timing after the timed region (profiling runs: "
+                         "keeps the trace's decoder dispatches to the pipeline's own)")
     ap.add_argument("--no-timeline", action="store_true",
                     help="native pipeline: no per-batch timing events in the timed run (the line's "
                          "config.stages is then null)")
@@ -955,6 +991,10 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
     """Everything after the timed region: host gather of the hypotheses,
     roofline, GEMM MFMA utilisation, CPU baseline and the JSON line (rank 0)."""
     d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout = weights
+    # per-stage spans, clock and CU placement of the timed run: top-level fields of the line
+    sched = dict(sched or {})
+    measured = {k: sched.pop(k) for k in ("stages", "clock", "cu_placement") if k in sched}
+    ser = sched.pop("serialized", None)
     DM = asr.DeviceMatrix.from_numpy
     # ---- host-side gather of the hypotheses (outside the timed region)
     labels, lens, lp = best
@@ -1027,6 +1067,15 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                 # that decode's wait for CUs; rocprofv3's dispatch duration of
                 # the same kernel in the committed trace of this workload:
                 "rocprof_kernel": kstats,
+                # the same kernel alone at the pipeline's load (live), and the
+                # chip-level rate: algorithmic bytes of a whole step / ms_per_step
+                "serialized": (dict(ser, achieved=round(bpf * Bl * T / (ser["ms_per_launch"] * 1e-3) / 1e9, 3),
+                                    frac=round(bpf * Bl * T / (ser["ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5))
+                               if ser else None),
+                "chip_level": {"achieved": round(bpf * GB * T * args.steps / elapsed / world / 1e9, 3),
+                               "frac": round(bpf * GB * T * args.steps / elapsed / world / 1e9 / HBM_PEAK_GBS, 5),
+                               "how": "algorithmic bytes of every frame decoded in the timed region / its "
+                                      "wall time, per GPU"},
                 "limiter": "on-chip dependency latency per frame (beam resident in LDS): "
                            "see roofline.issue for the measured issue/wait fractions"}
 
@@ -1064,9 +1113,6 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
                            best_p, full_T=args.cpu_full_T, emis_note=note)
         parity = cpu.pop("parity")
 
-    # per-stage spans, clock and CU placement of the timed run: top-level fields of the line
-    sched = dict(sched or {})
-    measured = {k: sched.pop(k) for k in ("stages", "clock", "cu_placement") if k in sched}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
@@ -1237,6 +1283,16 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
                             + ("yes" if same else "NO"))
         if not same:
             raise SystemExit("model_emissions does not reproduce the pipeline's emissions")
+    ser = None
+    if (rank == 0 and desc["mode"] == asr.PIPELINE_MODES[1] and desc["decode_cus"] < 256
+            and not args.no_serialized):
+        dc = desc["decode_cus"]
+        conc = max(1, (16 if kcap <= 64 else 9) * dc // Bp)   # the decodes the decode CUs hold
+        ms1 = serialized_decode(asr, em_last[0] if em_last is not None else pl.peek_emissions(), T, Bp, V, beam,
+                                dc, conc)
+        ser = {"ms_per_launch": round(ms1, 4), "concurrent": conc, "decode_cus": dc,
+               "how": f"{conc} decodes of the last batch's emissions at once on the {dc} decode CUs, "
+                      f"nothing else running (HIP events, live after the timed region)"}
     finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
            (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_last,
            {"pipeline_batch": Bp, "batches_per_step": nsub,
@@ -1245,13 +1301,14 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
             "segments": desc.get("segments"),
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
-            "stages": stages, "clock": clock_fig, "cu_placement": placement,
+            "stages": stages, "clock": clock_fig, "cu_placement": placement, "serialized": ser,
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
                         f"library-owned streams, buffers and decoder schedule"},
            parity_src=(Bp, (lab_p, ln_p, lp_p)))
     pl.close()
     asr.synchronize()
+    destroy_raw_streams()
 
 
 def greedy_host(T, V, first, count, seed=20261015):

@@ -16,12 +16,16 @@ set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_${OUT:-run}
 mkdir -p "$OUT"
-ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline --no-serialized"}
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 # the decoder's VALU mix (fp64 share, VALU issue cycles) and the scalar unit
 VALU="SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES"
 # matrix-core evidence of the dense kernels (+ the clock)
 # (fp32 MFMAs: the fp32 kernels and the emission GEMM; bf16 MFMAs: the split-bf16 kernels, dense_x3.hip)
+# where the decoder's waits go: LDS / VMEM / SMEM instruction
+# cycles and LDS bank conflicts; then the issue side
+WAIT="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_LDS_BANK_CONFLICT"
+ISSUE="SQ_IFETCH SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_BUSY_CYCLES"
 MFMA="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_BF16 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
 for pass in ${PASSES:-trace fetch write}; do
     case $pass in
@@ -38,6 +42,10 @@ for pass in ${PASSES:-trace fetch write}; do
                    -- python3 bench.py $ARGS > "$OUT/valu.log" 2>&1 ;;
         mfma)  timeout -s KILL 180 rocprofv3 --pmc $MFMA --output-format csv -d "$OUT/mfma" -o run \
                    -- python3 bench.py $ARGS > "$OUT/mfma.log" 2>&1 ;;
+        wait)  timeout -s KILL 180 rocprofv3 --pmc $WAIT --output-format csv -d "$OUT/wait" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/wait.log" 2>&1 ;;
+        issue) timeout -s KILL 180 rocprofv3 --pmc $ISSUE --output-format csv -d "$OUT/issue" -o run \
+                   -- python3 bench.py $ARGS > "$OUT/issue.log" 2>&1 ;;
         grbm)  timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/grbm" -o run \
                    -- python3 bench.py $ARGS > "$OUT/grbm.log" 2>&1 ;;
         *) echo "unknown pass $pass"; exit 2 ;;
