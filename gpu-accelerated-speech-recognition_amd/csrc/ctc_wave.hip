@@ -28,7 +28,7 @@ bool ctc_wave_supported(const CtcGeom& g, int cu_mode) {
 
 int ctc_launch_decode_wave(const CtcArgs& a, hipStream_t s) {
     // the emission prefetch addresses a chunk's elements by 32-bit offsets
-    if ((long)(wave_ch(a.g.V) - 1) * a.tstride + a.g.V >= 0x7fffffffL) return ASR_ERR_UNSUPPORTED;
+    if (((long)(wave_ch(a.g.V) - 1) * a.tstride + a.g.V) * 4 >= 0x7fffffffL) return ASR_ERR_UNSUPPORTED;
     const size_t lds = ctc_lds_bytes_wave(a.g);
     const dim3 grid(a.B), block(64);
     const bool c64 = a.g.V > 32;
