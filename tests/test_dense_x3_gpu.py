@@ -176,3 +176,42 @@ def test_emit_fp32_accuracy(T, B, H, V, arith):
     finally:
         asr.rnn_set_recurrence(asr.RNN_RECUR_AUTO)
     assert np.array_equal(hid2.toCpu(), hids[asr.DENSE_SPLIT_BF16])
+
+
+@pytest.mark.parametrize("B,H", [(16, 256), (48, 128)])
+def test_emit_fp32_accuracy_full_sequence(B, H, arith):
+    """the split-bf16 recurrence + emission over the
+    headline's whole T = 1000 (bench.py's weight scales: U(+-1/sqrt(H))
+    W_hh, U(+-4/sqrt(H)) W_out) against fp64: the error must not grow along
+    the sequence — emissions within 5e-6 and hidden states within 2e-6 at
+    every frame, no worse than the fp32 MFMA kernel (x 1.5 + 5e-7), and the
+    last 100 frames no worse than 2x the first 100."""
+    T, V = 1000, 29
+    rng = np.random.default_rng(B + H)
+    s = 1 / np.sqrt(H)
+    P = rng.uniform(-1, 1, (T, B, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    w_out = rng.uniform(-4 * s, 4 * s, (H, V)).astype(np.float32)
+    b_out = rng.uniform(-0.5, 0.5, V).astype(np.float32)
+    h64 = _rnn64(P, T, B, w_hh, b_hh.astype(np.float64) + b_ih.astype(np.float64))
+    z = h64 @ w_out.astype(np.float64) + b_out
+    z = z - z.max(axis=-1, keepdims=True)
+    eref = z - np.log(np.exp(z).sum(axis=-1, keepdims=True))
+    W = [dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1)), dm(w_out), dm(b_out.reshape(V, 1))]
+    err_e, err_h, per_frame = {}, {}, {}
+    for kind in (asr.DENSE_SPLIT_BF16, asr.DENSE_F32):
+        asr.set_dense_arith(kind)
+        em, hid = asr.DeviceMatrix(T * B, V), asr.DeviceMatrix(T * B, H)
+        asr.rnn_emit_fwd(*W, dm(P.reshape(T * B, H)), em, T, B, hid=hid)
+        d = np.abs(em.toCpu().reshape(T, B, V) - eref)
+        err_e[kind] = float(d.max())
+        per_frame[kind] = d.max(axis=(1, 2))
+        err_h[kind] = float(np.abs(hid.toCpu().reshape(T, B, H) - h64).max())
+    x3 = asr.DENSE_SPLIT_BF16
+    assert err_e[x3] <= 5e-6 and err_h[x3] <= 2e-6, (err_e, err_h)
+    assert err_e[x3] <= 1.5 * err_e[asr.DENSE_F32] + 5e-7, err_e
+    assert err_h[x3] <= 1.5 * err_h[asr.DENSE_F32] + 2e-7, err_h
+    assert per_frame[x3][-100:].max() <= 2 * per_frame[x3][:100].max() + 5e-7, \
+        (per_frame[x3][:100].max(), per_frame[x3][-100:].max())
