@@ -37,7 +37,7 @@ int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, 
 // hlast [B][H] (optional, may be h0): h_{T-1}, the h0 of a next segment.
 int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                          const float* P, float* hout, const float* Wout, const float* bout, float* emis,
-                         int T, int B, int H, int V, hipStream_t s, float* hlast = nullptr);
+                         int T, int B, int H, int V, hipStream_t s, float* hlast = nullptr, bool pfrag = false);
 int bias_tanh_launch(float* p, const float* b_ih, const float* b_hh, long n, int H, hipStream_t s);
 int axpy_launch(const float* x, const float* y, float* z, long n, float lam, hipStream_t s);
 int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);
@@ -64,9 +64,15 @@ int gemm_x3_launch(const GemmArgs& g, int epi, int tpw, hipStream_t s);
 bool rnn_x3_applies(int B, int H);
 int rnn_recur_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
                         int T, int B, int H, hipStream_t s);
+// pfrag: P in the fragment-major layout written by gemm_x3_frag_launch (B % 16 == 0).
 int rnn_emit_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, const float* P,
                        float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int H, int V,
-                       hipStream_t s, float* hlast);
+                       hipStream_t s, float* hlast, bool pfrag = false);
+// The input projection P = A.W (K <= 256, H = N <= 256, H % 32 == 0, M % 16 == 0)
+// stored in the fragment-major layout the split-bf16 recurrence reads with
+// two 16-byte loads per lane and step (rnn_emit_x3_launch(..., pfrag = true)).
+// Internal to the pipeline: the values are asr_linear_fwd's, the layout is not row-major.
+int gemm_x3_frag_launch(const float* A, const float* W, float* P, int M, int K, int H, int tpw, hipStream_t s);
 
 // Bidirectional RNN plumbing (H % 4 == 0, 16-B aligned buffers).
 int time_reverse_launch(float* p, int T, long n, hipStream_t s);

@@ -883,9 +883,10 @@ int rnn_recur_mfma_launch(const float* h0, const float* Whh, const float* b_ih, 
 
 int rnn_emit_mfma_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh,
                          const float* P, float* hout, const float* Wout, const float* bout, float* emis,
-                         int T, int B, int H, int V, hipStream_t s, float* hlast) {
+                         int T, int B, int H, int V, hipStream_t s, float* hlast, bool pfrag) {
     if (dense_x3_on() && rnn_x3_applies(B, H) && V >= 1 && V <= RE_VMAX)
-        return rnn_emit_x3_launch(h0, Whh, b_ih, b_hh, P, hout, Wout, bout, emis, T, B, H, V, s, hlast);
+        return rnn_emit_x3_launch(h0, Whh, b_ih, b_hh, P, hout, Wout, bout, emis, T, B, H, V, s, hlast, pfrag);
+    if (pfrag) return ASR_ERR_UNSUPPORTED;   // the fragment-major P layout is the split-bf16 kernel's
     if (H > RNN_HMAX || (H & 15) != 0 || B <= 0 || V < 1 || V > RE_VMAX) return ASR_ERR_UNSUPPORTED;
     if ((long)B * H > 0x7fffffffL) return ASR_ERR_UNSUPPORTED;   // 32-bit offsets within a step
     if (hlast)

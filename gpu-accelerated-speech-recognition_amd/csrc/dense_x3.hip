@@ -174,6 +174,15 @@ __device__ __forceinline__ void lds_barrier_x3() {
 constexpr int X3_ROWS = 16;
 constexpr int X3_WAVES = 8;
 constexpr int X3_NCOL = 32 * X3_WAVES;
+// Internal epilogue: C in the recurrence's fragment-major P layout (below,
+// rnn_recur_x3_kernel<..., PFR>): row tile q of C (rows 16q .. 16q + 15) is
+// the block C + 16 q N, and in it wave w's lane l keeps its 8 values
+// (rows 4 (l >> 4) + j, columns 32 w + 16 ct + (l & 15); element 4 ct + j)
+// at floats (64 w + l) * 8 .. + 7: two 16-byte stores per lane here, two
+// 16-byte loads per lane in the recurrence, instead of eight 4-byte ones
+// each.  N = H (one 256-column block, waves past N / 32 store nothing),
+// M % 16 == 0, no bias.
+constexpr int X3_EPI_FRAG = 8;
 
 template <int NCH>
 constexpr int x3_gemm_lds() {
@@ -305,6 +314,13 @@ __global__ __launch_bounds__(64 * X3_WAVES) void gemm_x3_kernel(GemmArgs g, int 
         stage(cur ^ 1);
         load(tile + 2 * tstep);
         const long r0 = (long)tile * X3_ROWS;
+        if (EPI == X3_EPI_FRAG) {
+            if (32 * w < g.N) {
+                f32x4* dst = reinterpret_cast<f32x4*>(g.C + r0 * g.N + (long)(64 * w + lane) * 8);
+                dst[0] = acc[0];
+                dst[1] = acc[1];
+            }
+        } else {
         const auto cs = brsrc(g.C + r0 * g.ldc, min((long)X3_ROWS, (long)g.M - r0) * g.ldc * 4);
 #pragma unroll
         for (int ct = 0; ct < 2; ct++) {
@@ -317,6 +333,7 @@ __global__ __launch_bounds__(64 * X3_WAVES) void gemm_x3_kernel(GemmArgs g, int 
                     bstore(cs, ((4 * gq + j) * (int)g.ldc + ncol[ct]) * 4, y);
                 }
             }
+        }
         }
         __syncthreads();
         cur ^= 1;
@@ -360,6 +377,17 @@ bool gemm_x3_applies(const GemmArgs& g, int epi) {
            (long)g.ldc * 4 * X3_ROWS < 0x7fffffffL;
 }
 
+int gemm_x3_frag_launch(const float* A, const float* W, float* P, int M, int K, int H, int tpw, hipStream_t s) {
+    GemmArgs g{};
+    g.A = A; g.B = W; g.C = P;
+    g.M = M; g.N = H; g.K = K;
+    g.sam = K; g.sak = 1; g.sbk = H; g.sbn = 1; g.ldc = H;
+    if (!gemm_x3_applies(g, EPI_NONE) || (M % X3_ROWS) != 0 || (H % 32) != 0 || H > X3_NCOL ||
+        ((uintptr_t)P % 16) != 0)
+        return ASR_ERR_UNSUPPORTED;
+    return launch_gemm_x3_epi<X3_EPI_FRAG>(g, tpw, s);
+}
+
 int gemm_x3_launch(const GemmArgs& g, int epi, int tpw, hipStream_t s) {
     if (!gemm_x3_applies(g, epi)) return ASR_ERR_UNSUPPORTED;
     switch (epi) {
@@ -396,7 +424,7 @@ constexpr int x3_recur_lds() {
     return 2 * 3 * 16 * (NCH * 32 + 8) * 2 + (EMIT ? 3 * NCH * 2 * 64 * 16 + 2 * NCH * 4 * 64 * 8 : 0);
 }
 
-template <int NCH, bool EMIT, bool HL>
+template <int NCH, bool EMIT, bool HL, bool PFR>
 __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
                                                                 const float* __restrict__ Whh,
                                                                 const float* __restrict__ b_ih,
@@ -476,14 +504,27 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
     int voff[2];
 #pragma unroll
     for (int ct = 0; ct < 2; ct++) voff[ct] = ((r0 + 4 * gq) * H + ncol[ct]) * 4;
+    // PFR: P in the fragment-major layout (X3_EPI_FRAG; B % 16 == 0): this
+    // lane's 8 values of a step are 32 contiguous bytes
+    const int poff = (blockIdx.x * 16 * H + (64 * w + lane) * 8) * 4;
     float pn[2][4];
-    {
-        const auto rs = brsrc(hid, slab);
+    auto pload = [&](const float* base) {
+        const auto rs = brsrc(base, slab);
+        if (PFR) {
 #pragma unroll
-        for (int ct = 0; ct < 2; ct++)
+            for (int ct = 0; ct < 2; ct++) {
+                const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, poff + 16 * ct, 0, 0));
 #pragma unroll
-            for (int j = 0; j < 4; j++) pn[ct][j] = bload(rs, voff[ct] + j * H * 4);
-    }
+                for (int j = 0; j < 4; j++) pn[ct][j] = v[j];
+            }
+        } else {
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) pn[ct][j] = bload(rs, voff[ct] + j * H * 4);
+        }
+    };
+    pload(hid);
     float* const hdst = EMIT ? hout : hid;
     // EMIT: partial of the h held in hs[buf] over k-chunk w
     auto emit_partial = [&](const __bf16* pb, f32x4 (&ea)[2]) {
@@ -559,13 +600,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
         for (int ct = 0; ct < 2; ct++)
 #pragma unroll
             for (int j = 0; j < 4; j++) p[ct][j] = pn[ct][j];
-        {
-            const auto rn = brsrc(hid + (t + 1 < T ? t + 1 : t) * tstride, slab);
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) pn[ct][j] = bload(rn, voff[ct] + j * H * 4);
-        }
+        pload(hid + (t + 1 < T ? t + 1 : t) * tstride);
         const __bf16* pb = hsb + cur * 3 * PIECE;
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -577,7 +612,8 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
             X3_PRODUCTS(2, acc, ah, am, al, bh, bm, bl, c)
         }
         __bf16* hn = hsb + (cur ^ 1) * 3 * PIECE;
-        const auto rs = brsrc(hdst + t * tstride, (!EMIT || hdst) ? slab : 0);
+        const bool sth = !EMIT || hdst != nullptr;   // EMIT without hout: the hidden states are not stored
+        const auto rs = brsrc(hdst + t * tstride, sth ? slab : 0);
 #if ASR_X3R_PACK
         // columns n and n + 16 are adjacent in the piece rows: one bf16 pair per piece and row
 #pragma unroll
@@ -587,7 +623,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
             for (int ct = 0; ct < 2; ct++) {
                 const float h = x3_tanh((p[ct][j] + acc[ct][j]) + bias[ct]);
                 split3(h, a[ct], b[ct], c[ct]);
-                bstore(rs, voff[ct] + j * H * 4, h);
+                if (sth) bstore(rs, voff[ct] + j * H * 4, h);
             }
             const int o = (4 * gq + j) * AS + 32 * w + 2 * c15;
             typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -607,7 +643,7 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
                 hn[o] = a;
                 hn[PIECE + o] = b;
                 hn[2 * PIECE + o] = c;
-                bstore(rs, voff[ct] + j * H * 4, h);
+                if (sth) bstore(rs, voff[ct] + j * H * 4, h);
             }
         }
 #endif
@@ -642,27 +678,27 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
     }
 }
 
-template <int NCH, bool EMIT, bool HL>
+template <int NCH, bool EMIT, bool HL, bool PFR>
 static int launch_recur_x3_k(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
                              float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int V,
                              float* hlast, hipStream_t s) {
     constexpr int lds = x3_recur_lds<NCH, EMIT>();
     static AsrAttrOnce attr;
-    if (int r_ = attr.set((const void*)rnn_recur_x3_kernel<NCH, EMIT, HL>, lds)) return r_;
-    hipLaunchKernelGGL((rnn_recur_x3_kernel<NCH, EMIT, HL>), dim3((unsigned)((B + 15) / 16)), dim3(64 * NCH), lds,
-                       s, h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast);
+    if (int r_ = attr.set((const void*)rnn_recur_x3_kernel<NCH, EMIT, HL, PFR>, lds)) return r_;
+    hipLaunchKernelGGL((rnn_recur_x3_kernel<NCH, EMIT, HL, PFR>), dim3((unsigned)((B + 15) / 16)), dim3(64 * NCH),
+                       lds, s, h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }
 
-template <bool EMIT, bool HL>
+template <bool EMIT, bool HL, bool PFR = false>
 static int launch_recur_x3(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
                            float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int H,
                            int V, float* hlast, hipStream_t s) {
     switch (H) {
-        case 64: return launch_recur_x3_k<2, EMIT, HL>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
-        case 128: return launch_recur_x3_k<4, EMIT, HL>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
-        case 256: return launch_recur_x3_k<8, EMIT, HL>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
+        case 64: return launch_recur_x3_k<2, EMIT, HL, PFR>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
+        case 128: return launch_recur_x3_k<4, EMIT, HL, PFR>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
+        case 256: return launch_recur_x3_k<8, EMIT, HL, PFR>(h0, Whh, b_ih, b_hh, hid, hout, Wout, bout, emis, T, B, V, hlast, s);
         default: return ASR_ERR_UNSUPPORTED;
     }
 }
@@ -680,8 +716,16 @@ int rnn_recur_x3_launch(const float* h0, const float* Whh, const float* b_ih, co
 
 int rnn_emit_x3_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, const float* P,
                        float* hout, const float* Wout, const float* bout, float* emis, int T, int B, int H, int V,
-                       hipStream_t s, float* hlast) {
+                       hipStream_t s, float* hlast, bool pfrag) {
     if (!rnn_x3_applies(B, H) || T <= 0 || V < 1 || V > RX_VMAX) return ASR_ERR_UNSUPPORTED;
+    if (pfrag) {   // P in the fragment-major layout of gemm_x3_frag_launch
+        if ((B % 16) != 0 || ((uintptr_t)P % 16) != 0) return ASR_ERR_UNSUPPORTED;
+        if (hlast)
+            return launch_recur_x3<true, true, true>(h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout,
+                                                     emis, T, B, H, V, hlast, s);
+        return launch_recur_x3<true, false, true>(h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout,
+                                                  emis, T, B, H, V, nullptr, s);
+    }
     if (hlast)
         return launch_recur_x3<true, true>(h0, Whh, b_ih, b_hh, const_cast<float*>(P), hout, Wout, bout, emis, T, B,
                                            H, V, hlast, s);

@@ -70,6 +70,12 @@ struct asr_pipeline {
     int ngroups = 1;      // CU groups of the decodes (GROUPS / GROUPS2): decode d on group d % ngroups
     bool split = false;   // GROUPS: input GEMM / recurrence / emission GEMM on two streams
     bool fuse = false;    // SHARED: recurrence + emission projection in one kernel (asr_rnn_emit_fwd)
+    // fused split-bf16 production: the input projection is stored in the
+    // recurrence's fragment-major layout (asr::gemm_x3_frag_launch: two
+    // 16-byte stores / loads per lane instead of eight 4-byte ones; the same
+    // values, so the same emission bits as asr_linear_fwd + asr_rnn_emit_fwd)
+    bool pfrag = false;
+    int ptiled = 0;       // production-side input projection: row tiles per workgroup (0: persistent)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
     int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
@@ -175,6 +181,17 @@ struct ArithGuard {
     ~ArithGuard() { asr_internal_dense_arith = prev; }
 };
 
+// The fused production's input projection of `rows` rows (x rows -> P rows):
+// fragment-major when the pipeline reads it so, else asr_linear_fwd.
+int input_projection(asr_pipeline* p, const float* x, float* P, long rows, int tiled, hipStream_t st) {
+    const auto& c = p->cfg;
+    if (p->pfrag) return asr::gemm_x3_frag_launch(x, p->W_ih, P, (int)rows, c.in, c.H, tiled, st);
+    asr_internal_gemm_tiled = tiled;
+    const int rc = asr_linear_fwd(x, p->W_ih, nullptr, P, (int)rows, c.in, c.H, ASR_EPI_NONE, st);
+    asr_internal_gemm_tiled = 0;
+    return rc;
+}
+
 // Production of batch i into buffer k (unsplit): RNN forward + emission projection.
 int produce_full(asr_pipeline* p, long i, const float* x) {
     const auto& c = p->cfg;
@@ -213,22 +230,18 @@ int produce_fused_segments(asr_pipeline* p, long i, const float* x, hipStream_t 
         const long r0 = (long)t0 * c.B, rows = (long)(t1 - t0) * c.B;
         const long ga = frac128 > 0 ? std::min(rows, frac128 * rows / ((long)c.T * c.B) / 128 * 128) : 0;
         if (ga > 0) {
-            asr_internal_gemm_tiled = p->gtiled;
-            rc = asr_linear_fwd(x + r0 * c.in, p->W_ih, nullptr, p->hid[k] + r0 * c.H, (int)ga, c.in, c.H,
-                                ASR_EPI_NONE, p->s_gdec);
-            asr_internal_gemm_tiled = 0;
+            rc = input_projection(p, x + r0 * c.in, p->hid[k] + r0 * c.H, ga, p->gtiled, p->s_gdec);
             if (rc) return rc;
             ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
         }
         if (ga < rows)
-            rc = asr_linear_fwd(x + (r0 + ga) * c.in, p->W_ih, nullptr, p->hid[k] + (r0 + ga) * c.H, (int)(rows - ga),
-                                c.in, c.H, ASR_EPI_NONE, sp);
+            rc = input_projection(p, x + (r0 + ga) * c.in, p->hid[k] + (r0 + ga) * c.H, rows - ga, p->ptiled, sp);
         if (rc) return rc;
         if (ga > 0) ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_proj[k], 0));
         rc = asr::rnn_emit_mfma_launch(s > 0 ? p->hst[k] : nullptr, p->W_hh, p->b_ih, p->b_hh,
                                        p->hid[k] + r0 * c.H, nullptr, p->W_out, p->b_out,
                                        p->emis[k] + (long)t0 * c.B * c.V, t1 - t0, c.B, c.H, c.V, sp,
-                                       s + 1 < p->S ? p->hst[k] : nullptr);
+                                       s + 1 < p->S ? p->hst[k] : nullptr, p->pfrag);
         if (rc) return rc;
         ASR_HIP_TRY(hipEventRecord(p->ev_seg[(size_t)k * p->S + s], sp));
     }
@@ -261,19 +274,17 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
         // with several decodes in flight the decode-side rows use the tiled
         // kernel: a decode launched meanwhile then waits at most one tile's
         // workgroups for its CUs, not a persistent workgroup's whole share
-        asr_internal_gemm_tiled = p->gtiled;
-        rc = asr_linear_fwd(x, p->W_ih, nullptr, p->hid[k], (int)ga, c.in, c.H, ASR_EPI_NONE, p->s_gdec);
-        asr_internal_gemm_tiled = 0;
+        rc = input_projection(p, x, p->hid[k], ga, p->gtiled, p->s_gdec);
         if (rc) return rc;
         ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
     }
-    if (ga < M)
-        rc = asr_linear_fwd(x + ga * c.in, p->W_ih, nullptr, p->hid[k] + ga * c.H, (int)(M - ga), c.in, c.H,
-                            ASR_EPI_NONE, sp);
+    if (ga < M) rc = input_projection(p, x + ga * c.in, p->hid[k] + ga * c.H, M - ga, p->ptiled, sp);
     if (rc) return rc;
     if (ga > 0) ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_proj[k], 0));
-    rc = asr_rnn_emit_fwd(nullptr, p->W_hh, p->b_ih, p->b_hh, p->W_out, p->b_out, p->hid[k], nullptr, p->emis[k],
-                          c.T, c.B, c.H, c.V, sp);
+    rc = p->pfrag ? asr::rnn_emit_mfma_launch(nullptr, p->W_hh, p->b_ih, p->b_hh, p->hid[k], nullptr, p->W_out,
+                                              p->b_out, p->emis[k], c.T, c.B, c.H, c.V, sp, nullptr, true)
+                  : asr_rnn_emit_fwd(nullptr, p->W_hh, p->b_ih, p->b_hh, p->W_out, p->b_out, p->hid[k], nullptr,
+                                     p->emis[k], c.T, c.B, c.H, c.V, sp);
     if (rc) return rc;
     if (int r = mark(p, 1, k, sp)) return r;
     ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
@@ -558,6 +569,7 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         return ASR_ERR_ARG;
     asr_pipeline* p = new asr_pipeline();
     p->cfg = c;
+    if (const char* t = getenv("ASR_PIPELINE_PTILED")) p->ptiled = std::max(0, atoi(t));   // A/B
     if (const char* f = getenv("ASR_PIPELINE_FAULT")) {   // test hook: "<batch>:<stage>"
         long b = -1;
         char st[8] = {0};
@@ -707,6 +719,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     if (p->fuse && p->mode == SHARED) {
         const int S = c.segments ? c.segments : auto_segments(c, kcap);
         p->S = std::max(1, std::min(S, c.T));
+    }
+    // fragment-major P between the input projection and the split-bf16 fused
+    // recurrence (ASR_PIPELINE_PFRAG=0: row-major, A/B)
+    {
+        const char* pf = getenv("ASR_PIPELINE_PFRAG");
+        p->pfrag = p->fuse && asr::dense_x3_on() && asr::rnn_x3_applies(c.B, c.H) && (c.B % 16) == 0 &&
+                   c.in <= 256 && (c.in % 4) == 0 && !(pf && atoi(pf) == 0);
     }
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
     // hardware queues (default 4, read when the runtime starts), and streams
