@@ -594,13 +594,22 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     const int kcap = (K + std::max(8, K / 8) + 31) / 32 * 32;
     const int bcu = (c.B + 7) / 8 * 8;   // CUs at one decode workgroup per utterance
     int occw = 0;                          // one-wave decoder workgroups per CU (SHARED)
-    if (c.H <= 256 && c.V + 1 <= 64 && 4 * bcu <= ncu) {
+    // Batches of 64 utterances or more take the chip-filling schedule (many
+    // one-wave decodes in flight on half of the CUs) even when one batch
+    // would fit a quarter of the CUs at one 8-wave workgroup per utterance:
+    // C2 (B = 64, T = 500), 20 steps / warmup 5: CU groups 51.8 M frames/s,
+    // chip-filling 67.5 M (10 decodes in flight; 6 / 12 / 16: 45.5 / 68.6 /
+    // 63.2 M; 192 decode CUs or 32 hardware queues: 20-48 M; runs sg, sh).
+    // ASR_PIPELINE_MODE=0 keeps the CU groups (A/B).
+    const char* fm = getenv("ASR_PIPELINE_MODE");
+    const bool small_shared = c.B >= 64 && !(fm && atoi(fm) == 0);
+    if (c.H <= 256 && c.V + 1 <= 64 && 4 * bcu <= ncu && !small_shared) {
         p->mode = GROUPS;
         p->gcu = bcu;
         p->D = c.inflight ? c.inflight : std::max(1, std::min(3, ncu / bcu - 1));
         p->P = 1;
         p->split = true;
-    } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 128 && 2 * bcu > ncu &&
+    } else if (c.H <= 256 && c.V + 1 <= 64 && kcap <= 128 && (2 * bcu > ncu || small_shared) &&
                (occw = wave_occupancy(c)) > 0) {
         p->mode = SHARED;
         p->rnn_kind = ASR_RNN_RECUR_MFMA;

@@ -16,21 +16,27 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _bench(*args, config="C2"):
+def _bench(*args, config="C2", env=None):
+    import os
     cmd = [sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", "--steps", "6", "--warmup", "2",
            "--T", "100", "--config", config, *args]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                         env=dict(os.environ, **(env or {})))
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
     return line
 
 
 def test_inflight_and_split_production_match_sequential():
+    """The CU-group schedules (ASR_PIPELINE_MODE=0 keeps C2's 64-utterance
+    batches on them) against the sequential loop: the same unfused production
+    (recurrence, then the emission GEMM), the same bits."""
+    groups = {"ASR_PIPELINE_MODE": "0"}
     seq = _bench("--no-pipeline")
     runs = {
         "packed": _bench("--packed"),   # 4-wave decode workgroups two to a CU, 5 batches in flight
-        "d1": _bench("--inflight", "1"),
-        "d3_split_all": _bench("--inflight", "3"),              # auto: production split, GEMMs on all CUs
+        "d1": _bench("--inflight", "1", env=groups),
+        "d3_split_all": _bench("--inflight", "3", env=groups),   # auto: production split, GEMMs on all CUs
         "d2_unsplit_graph": _bench("--inflight", "2", "--prod-split", "off", "--graph-production", "on",
                                    "--prod-streams", "2"),
     }
@@ -40,6 +46,19 @@ def test_inflight_and_split_production_match_sequential():
     assert runs["d3_split_all"]["config"]["inflight_decodes"] == 3
     assert runs["packed"]["config"]["decode_waves"] == 4 and runs["packed"]["config"]["inflight_decodes"] == 5
     assert runs["d2_unsplit_graph"]["config"]["production_streams"] == 2
+
+
+def test_c2_chip_filling_schedule_independent():
+    """C2's default native schedule (64-utterance batches on the chip-filling
+    schedule: one-wave decodes, 10 in flight, fused production) gathers the
+    same digest at 1, 3 and the default decodes in flight and with the
+    production in one T-segment — placement and overlap never change a bit."""
+    base = _bench()
+    assert base["config"]["inflight_decodes"] == 10 and base["config"]["decode_waves"] == -1, base["config"]
+    assert base["config"]["fused_emission"] is True
+    for args in (("--inflight", "1"), ("--inflight", "3"), ("--segments", "1")):
+        r = _bench(*args)
+        assert r["gather"] == base["gather"], args
 
 
 def test_c4_self_launched_ranks_match_one_rank():

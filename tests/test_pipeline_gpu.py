@@ -294,7 +294,7 @@ def _covers(pl, ncu):
 
 
 @pytest.mark.parametrize("T,B,inp,H,V,beam,mode", [
-    (24, 64, 64, 256, 29, 50, "CU groups (small batches)"),
+    (24, 48, 64, 256, 29, 50, "CU groups (small batches)"),
     (16, 32, 32, 384, 29, 8, "CU groups (H > 256)"),
 ])
 def test_pipeline_groups_fit_hw_queues(monkeypatch, T, B, inp, H, V, beam, mode):
