@@ -740,16 +740,25 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // hardware queues (default 4, read when the runtime starts), and streams
     // that share a queue run one after another (C5, 5 streams on 4 queues:
     // 1.03 M vs 3.48 M frames/s).  Fit the automatic schedule to the queues:
-    // fewer production streams first, then the decode CUs' share of the
-    // input projection, then fewer decodes in flight; explicit counts are
-    // kept as given.  asr_pipeline_get_streams reports the outcome.
+    // no decode-CU share of the input projection first, then fewer
+    // production streams and decodes in flight, the larger count first;
+    // explicit counts are kept as given.  asr_pipeline_get_streams reports
+    // the outcome.
     {
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         p->hw_queues = (q && atoi(q) > 0) ? atoi(q) : 4;
         auto nstreams = [&] { return p->D + p->P + (p->grows > 0 ? 1 : 0) + (p->split ? 1 : 0); };
-        while (nstreams() > p->hw_queues && !c.prod_streams && p->P > 1) p->P--;
         if (nstreams() > p->hw_queues && p->grows > 0) p->grows = 0;
-        while (nstreams() > p->hw_queues && !c.inflight && p->D > 1) p->D--;
+        // then production streams down to half the decodes in flight, then
+        // both (small batches need both: C2 at 8 queues as D = 7, P = 1 ran
+        // 16.4 M frames/s, at D = P = 4 38.7 M; at 16 queues D = 10, P = 6
+        // 61.3 M against D = P = 8 53.9 M; runs sn, sn2)
+        while (nstreams() > p->hw_queues) {
+            const bool canP = !c.prod_streams && p->P > 1, canD = !c.inflight && p->D > 1;
+            if (canP && (!canD || p->P > (p->D + 1) / 2)) p->P--;
+            else if (canD) p->D--;
+            else break;
+        }
         p->tail_own = p->split && nstreams() < p->hw_queues;
         p->streams = nstreams() + (p->tail_own ? 1 : 0);
     }
