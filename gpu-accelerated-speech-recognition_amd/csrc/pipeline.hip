@@ -75,7 +75,6 @@ struct asr_pipeline {
     // 16-byte stores / loads per lane instead of eight 4-byte ones; the same
     // values, so the same emission bits as asr_linear_fwd + asr_rnn_emit_fwd)
     bool pfrag = false;
-    int ptiled = 0;       // production-side input projection: row tiles per workgroup (0: persistent)
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
     int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
@@ -235,7 +234,7 @@ int produce_fused_segments(asr_pipeline* p, long i, const float* x, hipStream_t 
             ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
         }
         if (ga < rows)
-            rc = input_projection(p, x + (r0 + ga) * c.in, p->hid[k] + (r0 + ga) * c.H, rows - ga, p->ptiled, sp);
+            rc = input_projection(p, x + (r0 + ga) * c.in, p->hid[k] + (r0 + ga) * c.H, rows - ga, 0, sp);
         if (rc) return rc;
         if (ga > 0) ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_proj[k], 0));
         rc = asr::rnn_emit_mfma_launch(s > 0 ? p->hst[k] : nullptr, p->W_hh, p->b_ih, p->b_hh,
@@ -278,7 +277,7 @@ int produce_fused(asr_pipeline* p, long i, const float* x) {
         if (rc) return rc;
         ASR_HIP_TRY(hipEventRecord(p->ev_proj[k], p->s_gdec));
     }
-    if (ga < M) rc = input_projection(p, x + ga * c.in, p->hid[k] + ga * c.H, M - ga, p->ptiled, sp);
+    if (ga < M) rc = input_projection(p, x + ga * c.in, p->hid[k] + ga * c.H, M - ga, 0, sp);
     if (rc) return rc;
     if (ga > 0) ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_proj[k], 0));
     rc = p->pfrag ? asr::rnn_emit_mfma_launch(nullptr, p->W_hh, p->b_ih, p->b_hh, p->hid[k], nullptr, p->W_out,
@@ -569,7 +568,6 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         return ASR_ERR_ARG;
     asr_pipeline* p = new asr_pipeline();
     p->cfg = c;
-    if (const char* t = getenv("ASR_PIPELINE_PTILED")) p->ptiled = std::max(0, atoi(t));   // A/B
     if (const char* f = getenv("ASR_PIPELINE_FAULT")) {   // test hook: "<batch>:<stage>"
         long b = -1;
         char st[8] = {0};
@@ -730,12 +728,10 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->S = std::max(1, std::min(S, c.T));
     }
     // fragment-major P between the input projection and the split-bf16 fused
-    // recurrence (ASR_PIPELINE_PFRAG=0: row-major, A/B)
-    {
-        const char* pf = getenv("ASR_PIPELINE_PFRAG");
-        p->pfrag = p->fuse && asr::dense_x3_on() && asr::rnn_x3_applies(c.B, c.H) && (c.B % 16) == 0 &&
-                   c.in <= 256 && (c.in % 4) == 0 && !(pf && atoi(pf) == 0);
-    }
+    // recurrence (measured against row-major P: production ~2-3 % shorter,
+    // the same emission bits; run se)
+    p->pfrag = p->fuse && asr::dense_x3_on() && asr::rnn_x3_applies(c.B, c.H) && (c.B % 16) == 0 &&
+               c.in <= 256 && (c.in % 4) == 0;
     // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
     // hardware queues (default 4, read when the runtime starts), and streams
     // that share a queue run one after another (C5, 5 streams on 4 queues:
