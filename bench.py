@@ -545,6 +545,9 @@ def main():
     ap.add_argument("--no-serialized", action="store_true",
                     help="skip the live stand-alone decoder timing after the timed region (profiling runs: "
                          "keeps the trace's decoder dispatches to the pipeline's own)")
+    ap.add_argument("--prime-s", type=float, default=0.3,
+                    help="native pipeline: seconds of untimed steps before the W warmup steps (the clocks "
+                         "settle under the load; 0 = none)")
     ap.add_argument("--no-timeline", action="store_true",
                     help="native pipeline: no per-batch timing events in the timed run (the line's "
                          "config.stages is then null)")
@@ -1215,6 +1218,11 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     take.wait = 0.0
 
     run(-(-(2 * (desc["inflight"] + desc["prod_streams"]) + 1) // nsub))   # every buffer, stream and workspace once
+    # priming: the GPU's clocks settle under this load before the W warmup
+    # steps (untimed, like the line above; --prime-s 0 skips it)
+    tp = time.perf_counter()
+    while time.perf_counter() - tp < args.prime_s:
+        run(1)
     run(args.warmup)
     kernel_ms.clear()
     timeline = not args.no_timeline
