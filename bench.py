@@ -545,7 +545,7 @@ def main():
     ap.add_argument("--no-serialized", action="store_true",
                     help="skip the live stand-alone decoder timing after the timed region (profiling runs: "
                          "keeps the trace's decoder dispatches to the pipeline's own)")
-    ap.add_argument("--prime-s", type=float, default=0.3,
+    ap.add_argument("--prime-s", type=float, default=0.0,
                     help="native pipeline: seconds of untimed steps before the W warmup steps (the clocks "
                          "settle under the load; 0 = none)")
     ap.add_argument("--no-timeline", action="store_true",
