@@ -546,8 +546,8 @@ def main():
                     help="skip the live stand-alone decoder timing after the timed region (profiling runs: "
                          "keeps the trace's decoder dispatches to the pipeline's own)")
     ap.add_argument("--prime-s", type=float, default=0.0,
-                    help="native pipeline: seconds of untimed steps before the W warmup steps (the clocks "
-                         "settle under the load; 0 = none)")
+                    help="native pipeline: seconds of untimed steps before the W warmup steps (for the clocks "
+                         "to settle under the load; measured no effect at C4 / 256 per GPU, run ss)")
     ap.add_argument("--no-timeline", action="store_true",
                     help="native pipeline: no per-batch timing events in the timed run (the line's "
                          "config.stages is then null)")
