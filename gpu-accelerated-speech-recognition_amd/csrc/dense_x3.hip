@@ -58,9 +58,6 @@ bool dense_x3_on() { return dense_arith() == ASR_DENSE_SPLIT_BF16; }
 #ifndef ASR_X3R_TANH
 #define ASR_X3R_TANH 0   // recurrence: branch-free exp2 / rcp tanh (<= 1.6 ulp)
 #endif
-#ifndef ASR_X3R_SPLITCT
-#define ASR_X3R_SPLITCT 0   // recurrence: column tile 0's chain first, its epilogue among tile 1's MFMAs
-#endif
 #ifndef ASR_X3R_PACK
 #define ASR_X3R_PACK 0   // recurrence: k order permuted in each 32-chunk, h pieces written as bf16 pairs
 #endif
@@ -606,43 +603,6 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
         pload(hid + (t + 1 < T ? t + 1 : t) * tstride);
         const __bf16* pb = hsb + cur * 3 * PIECE;
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        __bf16* hn = hsb + (cur ^ 1) * 3 * PIECE;
-        const bool sth = !EMIT || hdst != nullptr;   // EMIT without hout: the hidden states are not stored
-        const auto rs = brsrc(hdst + t * tstride, sth ? slab : 0);
-#if ASR_X3R_SPLITCT && !ASR_X3R_PACK
-        // the same products in the same order per accumulator (each chain is
-        // its own: bits unchanged), tile 0's chain first; then tile 1's, with
-        // tile 0's epilogue (tanh, split, LDS and global stores) between its
-        // MFMAs — the vector ALU works while the matrix core does.  The A
-        // fragments are read twice (48 instead of 24 ds_read_b128 per step).
-        auto epi = [&](int ct, int j) {
-            const float h = x3_tanh((p[ct][j] + acc[ct][j]) + bias[ct]);
-            __bf16 a, b, c;
-            split3(h, a, b, c);
-            const int o = (4 * gq + j) * AS + ncol[ct];
-            hn[o] = a;
-            hn[PIECE + o] = b;
-            hn[2 * PIECE + o] = c;
-            if (sth) bstore(rs, voff[ct] + j * H * 4, h);
-        };
-#pragma unroll
-        for (int ct = 0; ct < 2; ct++) {
-            __asm__ volatile("" ::: "memory");   // re-read the fragments: no 96 live registers of them
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                const int off = c15 * AS + 32 * c + 8 * gq;
-                const bf16x8 ah = *reinterpret_cast<const bf16x8*>(pb + off);
-                const bf16x8 am = *reinterpret_cast<const bf16x8*>(pb + PIECE + off);
-                const bf16x8 al = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
-                f32x4 a1[1] = {acc[ct]};
-                X3_PRODUCTS(1, a1, ah, am, al, (bh + ct), (bm + ct), (bl + ct), c)
-                acc[ct] = a1[0];
-                if (ct == 1 && (c & 1) && (c >> 1) < 4) epi(0, c >> 1);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) epi(1, j);
-#else
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int off = c15 * AS + 32 * c + 8 * gq;
@@ -651,10 +611,10 @@ __global__ __launch_bounds__(64 * NCH) void rnn_recur_x3_kernel(const float* h0,
             const bf16x8 al = *reinterpret_cast<const bf16x8*>(pb + 2 * PIECE + off);
             X3_PRODUCTS(2, acc, ah, am, al, bh, bm, bl, c)
         }
-#endif
-#if ASR_X3R_SPLITCT && !ASR_X3R_PACK
-        // (epilogue done above)
-#elif ASR_X3R_PACK
+        __bf16* hn = hsb + (cur ^ 1) * 3 * PIECE;
+        const bool sth = !EMIT || hdst != nullptr;   // EMIT without hout: the hidden states are not stored
+        const auto rs = brsrc(hdst + t * tstride, sth ? slab : 0);
+#if ASR_X3R_PACK
         // columns n and n + 16 are adjacent in the piece rows: one bf16 pair per piece and row
 #pragma unroll
         for (int j = 0; j < 4; j++) {
