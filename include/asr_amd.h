@@ -396,12 +396,13 @@ int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode
 /* Streams the pipeline created and the process's HIP hardware queues
  * (GPU_MAX_HW_QUEUES as read at create; HIP's default is 4).  HIP maps
  * streams round-robin onto the queues and streams that share a queue
- * serialise, so the automatic schedule is fitted to the queues (fewer
- * production streams, then no input-projection share on the decode CUs,
- * then fewer decodes in flight; the small-batch mode's emission GEMMs get
- * a stream of their own only when a queue is left for it); streams >
- * hw_queues only when the caller fixed inflight / prod_streams.  DESIGN.md
- * §7c gives the measured cost. */
+ * serialise, so the automatic schedule is fitted to the queues (no
+ * input-projection share on the decode CUs, then fewer production streams
+ * down to half the decodes in flight, then both; the small-batch mode's
+ * emission GEMMs get a stream of their own only when a queue is left for
+ * it); streams > hw_queues only when the caller fixed inflight /
+ * prod_streams.  A server should export GPU_MAX_HW_QUEUES=24 (>= 16) before
+ * HIP starts: the measured cost of fewer queues is in INTEGRATION.md §3. */
 int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues);
 /* Where the pipeline's streams run: for each stream it created, its role
  * (ASR_PIPE_ROLE_*) and the CU range [cu_lo, cu_hi) of its CU mask
@@ -416,7 +417,8 @@ int asr_pipeline_get_placement(asr_pipeline_t* p, int cap, int* n, int* role, in
  * 8192 short workgroups on that stream that read HW_REG_XCC_ID / HW_REG_HW_ID
  * (synchronises the stream).  Workgroups are dealt round-robin over the XCDs
  * whatever the mask, so a role runs evenly only when its mask holds the same
- * number of CUs in every XCD; DESIGN.md §7f. */
+ * number of CUs in every XCD (mask bit i lands on XCD i % 8; an XCD the mask
+ * leaves out gets all of its CUs); DESIGN.md §10c. */
 int asr_pipeline_probe_placement(asr_pipeline_t* p, int role, int* cus_per_xcc, int* n_xcc);
 /* The emissions [T][B][V] (log-probabilities, device) that the decode of the
  * batch last returned by asr_pipeline_collect consumed — the exact bytes, for
