@@ -60,6 +60,10 @@ extern thread_local int asr_internal_gemm_tiled;
 // recurrence launches (H > 256) into the library's HIP graph at their first
 // use, not the second (a pipeline's buffers recur; one-off calls stay eager).
 extern thread_local int asr_internal_graph_now;
+// Set by the pipeline around its productions: the CUs one recurrence may
+// count on (its production streams' CU share), for the one-launch H > 256
+// recurrence whose workgroups must all be resident (0: no hint).
+extern thread_local int asr_internal_persist_cus;
 // Dense arithmetic for this thread's next dense calls (ASR_DENSE_*; -1: the
 // process-wide asr_set_dense_arith setting).  A pipeline latches the setting
 // it was created under and sets this around its own calls, so a later change

@@ -75,6 +75,7 @@ constexpr int WIDE_VMAX = 4096;   // largest vocabulary of the wide kernel (ctc_
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
 size_t ctc_tile0_bytes(int B, int T);   // a.tile0 workspace of the wide kernel
 size_t ctc_lds_bytes_wide(int kc, int V);
+size_t ctc_seg_bytes_wide(int kc);   // saved beam per utterance between segments (wide kernel)
 int ctc_set_max_lds_wide();
 // One wave per utterance (ctc_wave_kernel.inc): batches of many utterances per CU.
 size_t ctc_lds_bytes_wave(const CtcGeom& g);

@@ -10,8 +10,9 @@ size_t ctc_tile0_bytes(int B, int T) { return sizeof(uint32_t) * WREC * (size_t)
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s) {
     if (a.tile0) {   // every frame's first tile (ctc_tile0_kernel), then the decode
         if (a.g.V - 1 <= WTILE || a.g.V > WVMAX) return ASR_ERR_ARG;
-        hipLaunchKernelGGL(ctc_tile0_kernel, dim3((unsigned)(a.B * a.T)), dim3(64), sizeof(uint32_t) * a.g.V, s, a,
-                           a.tile0);
+        // the launch's frames [t0, t1) (a segment of a segmented decode)
+        hipLaunchKernelGGL(ctc_tile0_kernel, dim3((unsigned)(a.B * (a.t1 - a.t0))), dim3(64), sizeof(uint32_t) * a.g.V,
+                           s, a, a.tile0);
         ASR_LAUNCH_TRY();
     }
     const size_t lds = ctc_lds_bytes(a.g);
@@ -28,6 +29,14 @@ int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s) {
     ASR_W_LAUNCH(4)
 #undef ASR_W_LAUNCH
     return ASR_ERR_UNSUPPORTED;
+}
+
+size_t ctc_seg_bytes_wide(int kc) {
+    switch (kc) {
+    case 64: return LdsW<64>::SEG;
+    case 128: return LdsW<128>::SEG;
+    default: return LdsW<256>::SEG;
+    }
 }
 
 size_t ctc_lds_bytes_wide(int kc, int V) {

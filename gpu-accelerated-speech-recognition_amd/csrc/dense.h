@@ -44,6 +44,15 @@ int row_logsoftmax_launch(float* C, long ldc, int M, int N, hipStream_t s);
 // MFMA recurrence step (H % 128 == 0); ASR_ERR_UNSUPPORTED otherwise.
 int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const float* b_ih,
                          const float* b_hh, int B, int H, hipStream_t s);
+// The whole H > 256 recurrence in one launch with W_hh in registers and the
+// workgroups handing h_t to each other in memory (same bits as the step
+// launches); ASR_ERR_UNSUPPORTED outside 384 <= H <= 1024, H % 128 == 0,
+// B <= 256, or when its (H / 32) x ceil(B / 16) workgroups exceed `cus`
+// (the CUs the caller's stream gives this launch; <= 0: half of the device).
+int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                             int T, int B, int H, int cus, hipStream_t s);
+// 1 when a persistent recurrence gave up waiting (0.5 s without progress).
+int rnn_persist_status(int* timed_out);
 constexpr int STEP_MAXB = 4;
 // The same step for nb <= STEP_MAXB batches of B rows at once (one launch; batch j:
 // h_t at hts[j], h_{t-1} at hps[j]); nb > 1 needs B % 16 == 0.  Same bits.

@@ -1130,6 +1130,214 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 }
 
 // ---------------------------------------------------------------------------
+// The whole H > 256 recurrence in ONE launch (C5: B = 32, H = 1024, T =
+// 2000), replacing the T step launches above with the same bits: every
+// workgroup is the step kernel's (16 RB x 16 NT) tile with its 8-way K split,
+// but its W_hh slice (K/8 x 16 NT floats per wave: 64 VGPRs at H = 1024, NT
+// = 2) stays in registers for all T frames, and the workgroups hand h_t to
+// each other through memory inside the launch:
+//   * h_t is stored write-through (buffer stores with the sc1 bit) into hid
+//     (its final place); every storing wave drains its stores (vmcnt(0)),
+//     the workgroup barriers, and one lane adds 1 to a step counter
+//     (agent-scope atomic);
+//   * before frame t a workgroup's first lane polls the counter (agent-scope
+//     relaxed loads, s_sleep between) until all nWG workgroups have
+//     published frame t - 1, the workgroup barriers, and every load of
+//     h_{t-1} (and of P_t) is a buffer load with the sc1 bit (not served
+//     from this CU's L1) — the hand-off form of cdna_hip_programming.md §6
+//     Guideline 16 (one workgroup per CU: the launch requests more than half
+//     of a CU's LDS).
+// Every workgroup must be resident at once: the launcher only takes grids of
+// at most `cus` workgroups (the CUs the caller's stream may use), and a
+// bounded spin (0.5 s without progress) ends the kernel with an error flag
+// (asr::rnn_persist_status) instead of hanging.
+// The arithmetic per output is the step kernel's: each wave's K slice in
+// chunk order (4 MFMAs per 16-k chunk, k = 16 i + 4 g + j), the 8 partials
+// summed in wave order, tanhf((P_t + hh) + (b_hh + b_ih)); frame 0 without
+// h0 is bias_tanh's tanhf(P_0 + (b_hh + b_ih)).
+__device__ int g_rnn_persist_timeout = 0;
+constexpr int RP_LDS = 96 * 1024;   // one workgroup per CU
+constexpr int RP_SC1 = 16;          // buffer-instruction cache policy: sc1 (write-through / coherent)
+
+template <int RB, int NT, int KCH>
+__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const float* h0,
+                                                                          const float* __restrict__ Whh,
+                                                                          const float* __restrict__ b_ih,
+                                                                          const float* __restrict__ b_hh,
+                                                                          float* hid, int T, int B, int H,
+                                                                          unsigned* ctr) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 rp_part[];   // [RSM_WAVES][RB * NT][64], then the abort flag
+    int& rp_abort = *reinterpret_cast<int*>(rp_part + RSM_WAVES * RB * NT * 64);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    const int n0 = blockIdx.x * (16 * NT), r0 = blockIdx.y * (16 * RB);
+    const unsigned nwg = gridDim.x * gridDim.y;
+    const int kbeg = w * (H / RSM_WAVES);
+    // this wave's W_hh slice: chunk i, tile nt, MFMA j -> W[kbeg + 16 i + 4 g + j][n0 + 16 nt + c]
+    float bw[KCH][NT][4];
+#pragma unroll
+    for (int i = 0; i < KCH; i++)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) bw[i][nt][j] = Whh[(long)(kbeg + 16 * i + 4 * g + j) * H + n0 + 16 * nt + c];
+    int arow[RB];   // row offsets (floats) of this lane's A rows: rows past B read row B - 1 (never stored)
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) arow[rb] = min(r0 + rb * 16 + c, B - 1) * H + kbeg + 4 * g;
+    if (tid == 0) rp_abort = 0;
+    const long slab = (long)B * H;
+    const int sbytes = (int)(slab * 4);
+    for (int t = 0; t < T; t++) {
+        float* ht = hid + (long)t * slab;
+        const float* hp = t > 0 ? hid + (long)(t - 1) * slab : h0;
+        if (t > 0) {   // every workgroup has published frame t - 1
+            if (tid == 0) {
+                const unsigned target = nwg * (unsigned)t;
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s at 100 MHz
+                        rp_abort = 1;
+                        __hip_atomic_store(&g_rnn_persist_timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            if (rp_abort) return;
+        }
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(ht, (short)0, sbytes, 0x00020000);
+        if (hp) {
+            const auto rs_p = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hp), (short)0, sbytes, 0x00020000);
+            f32x4 acc[RB][NT];
+#pragma unroll
+            for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+                for (int nt = 0; nt < NT; nt++) acc[rb][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 a[KCH][RB];
+#pragma unroll
+            for (int i = 0; i < KCH; i++)
+#pragma unroll
+                for (int rb = 0; rb < RB; rb++)
+                    a[i][rb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             rs_p, (arow[rb] + 16 * i) * 4, 0, RP_SC1));
+#pragma unroll
+            for (int i = 0; i < KCH; i++)
+#pragma unroll
+                for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+                    for (int nt = 0; nt < NT; nt++) {
+                        f32x4& q = acc[rb][nt];
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].x, bw[i][nt][0], q, 0, 0, 0);
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].y, bw[i][nt][1], q, 0, 0, 0);
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].z, bw[i][nt][2], q, 0, 0, 0);
+                        q = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rb].w, bw[i][nt][3], q, 0, 0, 0);
+                    }
+#pragma unroll
+            for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+                for (int nt = 0; nt < NT; nt++) rp_part[(w * RB * NT + rb * NT + nt) * 64 + lane] = acc[rb][nt];
+            __syncthreads();
+            for (int e = tid; e < RB * NT * 256; e += 64 * RSM_WAVES) {
+                const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
+                const int rb = tl / NT, nt = tl - rb * NT;
+                const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
+                float hh = rp_part[tl * 64 + l][j];
+#pragma unroll
+                for (int q = 1; q < RSM_WAVES; q++) hh += rp_part[(q * RB * NT + tl) * 64 + l][j];
+                const int off = (r * H + n) * 4;   // rows past B: past the resource (load 0, store dropped)
+                const float P = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_t, off, 0, RP_SC1));
+                const float y = tanhf((P + hh) + (b_hh[n] + b_ih[n]));
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, off, 0, RP_SC1);
+            }
+        } else {   // h_{-1} = 0: bias_tanh's formula
+            for (int e = tid; e < RB * NT * 256; e += 64 * RSM_WAVES) {
+                const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
+                const int rb = tl / NT, nt = tl - rb * NT;
+                const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
+                const int off = (r * H + n) * 4;
+                const float P = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_t, off, 0, RP_SC1));
+                const float y = tanhf(P + (b_hh[n] + b_ih[n]));
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, off, 0, RP_SC1);
+            }
+        }
+        // publish frame t: every wave's stores drained, then one add per workgroup
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int RB, int NT, int KCH>
+static int launch_persist(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                          int T, int B, int H, unsigned* ctr, hipStream_t s) {
+    static AsrAttrOnce attr;
+    if (int r_ = attr.set((const void*)rnn_recur_persist_kernel<RB, NT, KCH>, RP_LDS)) return r_;
+    hipLaunchKernelGGL((rnn_recur_persist_kernel<RB, NT, KCH>), dim3((unsigned)(H / (16 * NT)), (unsigned)((B + 16 * RB - 1) / (16 * RB))),
+                       dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh, b_ih, b_hh, hid, T, B, H, ctr);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
+// Step counters, one per launch in flight (a ring; zeroed on the stream
+// before each launch).
+static int persist_counter(hipStream_t s, unsigned** out) {
+    static std::mutex mu;
+    static unsigned* ring[16] = {};
+    static unsigned next[16] = {};
+    int dev = 0;
+    ASR_HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 16) return ASR_ERR_UNSUPPORTED;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!ring[dev]) {
+        void* p = nullptr;
+        ASR_HIP_TRY(hipMalloc(&p, 64 * 256));
+        ASR_HIP_TRY(hipMemset(p, 0, 64 * 256));
+        ring[dev] = static_cast<unsigned*>(p);
+    }
+    unsigned* c = ring[dev] + 16 * (next[dev]++ % 64);   // 64-byte slots
+    ASR_HIP_TRY(hipMemsetAsync(c, 0, 16, s));
+    *out = c;
+    return ASR_OK;
+}
+
+int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
+                             int T, int B, int H, int cus, hipStream_t s) {
+    // cus: the CUs this launch may count on (its share of the stream's CU mask); <= 0: none given
+    // tiles: 16 x 32 (NT = 2); 256 rows at most; H / 128 chunks of 16 k per wave
+    const char* e = getenv("ASR_RNN_PERSIST");
+    if (e && e[0] == '0') return ASR_ERR_UNSUPPORTED;
+    if (T < 2 || B <= 0 || B > 256 || (H % 128) != 0 || H < 384 || H > 1024 || ((uintptr_t)hid % 16) != 0 ||
+        (h0 && ((uintptr_t)h0 % 16) != 0) || (long)B * H * 4 >= 0x7fffffffL)
+        return ASR_ERR_UNSUPPORTED;
+    const int nwg = (H / 32) * ((B + 15) / 16);
+    if (cus <= 0) {   // no hint: half of the device's CUs (room beside it)
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return ASR_ERR_UNSUPPORTED;
+        cus = ncu / 2;
+    }
+    if (nwg > cus) return ASR_ERR_UNSUPPORTED;   // every workgroup resident at once
+    unsigned* ctr = nullptr;
+    if (int rc = persist_counter(s, &ctr)) return rc;
+    switch (H / 128) {
+        case 3: return launch_persist<1, 2, 3>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+        case 4: return launch_persist<1, 2, 4>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+        case 5: return launch_persist<1, 2, 5>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+        case 6: return launch_persist<1, 2, 6>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+        case 7: return launch_persist<1, 2, 7>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+        default: return launch_persist<1, 2, 8>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+    }
+}
+
+int rnn_persist_status(int* timed_out) {
+    int v = 0;
+    ASR_HIP_TRY(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_rnn_persist_timeout), sizeof(int)));
+    *timed_out = v;
+    return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // In-place log_softmax of each row of C[M][ldc] (first N columns): one wave
 // per row, max and sum of exp by shuffle reductions.
 __global__ __launch_bounds__(256) void row_logsoftmax_kernel(float* __restrict__ C, long ldc, int M,

@@ -78,6 +78,7 @@ struct asr_pipeline {
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
     int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
+    int pcus = 0;         // CUs one production stream's recurrence may count on (one-launch H > 256 recurrence)
     int G = 1;            // GROUPS2: batches whose recurrences run as one (a production group)
     std::vector<long> group;          // batches whose input projection is queued, recurrence not yet
     std::vector<float*> hst;          // [nbuf][B][H] the recurrence's h at a segment end
@@ -191,6 +192,40 @@ int input_projection(asr_pipeline* p, const float* x, float* P, long rows, int t
     return rc;
 }
 
+// The unfused production in S T-segments (H > 256 with the wide decoder:
+// C5): segment s is its rows of the input projection, the recurrence over
+// its frames from h_{t0-1} (the previous segment's last hidden rows), and its
+// rows of the emission projection + log_softmax; event ev_seg[k][s] releases
+// the decode of those frames.  Rows and frames are independent and the
+// kernels are chosen by shape, not M: the unsegmented production's bits.
+int produce_full_segments(asr_pipeline* p, long i, const float* x, hipStream_t sp) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    int rc = ASR_OK;
+    for (int s = 0; s < p->S && !rc; s++) {
+        const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
+        const long r0 = (long)t0 * c.B, rows = (long)(t1 - t0) * c.B;
+        float* hs = p->hid[k] + r0 * c.H;
+        rc = asr_linear_fwd(x + r0 * c.in, p->W_ih, nullptr, hs, (int)rows, c.in, c.H, ASR_EPI_NONE, sp);
+        if (rc) return rc;
+        asr_internal_rnn_kind = p->rnn_kind;
+        asr_internal_graph_now = 1;
+        asr_internal_persist_cus = p->pcus;
+        rc = asr_rnn_recur_fwd(s > 0 ? hs - (long)c.B * c.H : nullptr, p->W_hh, p->b_ih, p->b_hh, hs, t1 - t0, c.B,
+                               c.H, sp);
+        asr_internal_persist_cus = 0;
+        asr_internal_graph_now = 0;
+        asr_internal_rnn_kind = -1;
+        if (!rc) rc = asr_linear_fwd(hs, p->W_out, p->b_out, p->emis[k] + r0 * c.V, (int)rows, c.H, c.V,
+                                     ASR_EPI_BIAS_LOGSOFTMAX, sp);
+        if (rc) return rc;
+        ASR_HIP_TRY(hipEventRecord(p->ev_seg[(size_t)k * p->S + s], sp));
+    }
+    if (int r = mark(p, 1, k, sp)) return r;
+    ASR_HIP_TRY(hipEventRecord(p->ev_ready[k], sp));
+    return ASR_OK;
+}
+
 // Production of batch i into buffer k (unsplit): RNN forward + emission projection.
 int produce_full(asr_pipeline* p, long i, const float* x) {
     const auto& c = p->cfg;
@@ -199,9 +234,12 @@ int produce_full(asr_pipeline* p, long i, const float* x) {
     if (fault(p, i, "produce")) return ASR_ERR_INTERNAL;
     ASR_HIP_TRY(hipStreamWaitEvent(sp, p->ev_free[k], 0));   // the decode reading this buffer is done
     if (int r = mark(p, 0, k, sp)) return r;
+    if (p->S > 1) return produce_full_segments(p, i, x, sp);
     asr_internal_rnn_kind = p->rnn_kind;
     asr_internal_graph_now = 1;
+    asr_internal_persist_cus = p->pcus;
     int rc = asr_rnn_fwd(x, nullptr, p->W_ih, p->W_hh, p->b_ih, p->b_hh, p->hid[k], c.T, c.B, c.in, c.H, sp);
+    asr_internal_persist_cus = 0;
     asr_internal_graph_now = 0;
     asr_internal_rnn_kind = -1;
     if (!rc) rc = asr_linear_fwd(p->hid[k], p->W_out, p->b_out, p->emis[k], c.T * c.B, c.H, c.V,
@@ -446,6 +484,14 @@ int fetch_to(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, do
     asr_ctc_t* h = p->dec[j % p->nbuf];
     *res_rc = asr_ctc_get_best(h, labels, max_len, lengths, logp);
     if (*res_rc != ASR_OK && *res_rc != ASR_ERR_BEAM_OVERFLOW) return *res_rc;
+    if (p->cfg.H > 256) {   // a one-launch recurrence that gave up waiting for its workgroups (never expected)
+        int timed_out = 0;
+        if (int r = asr::rnn_persist_status(&timed_out)) return r;
+        if (timed_out) {
+            set_failed(p, j, ASR_ERR_INTERNAL);
+            return ASR_ERR_INTERNAL;
+        }
+    }
     if (ms) asr_ctc_last_kernel_ms(h, ms);
     if (p->timing && j >= p->timing_from) {   // the batch's stamps, all complete once its decode is
         const int k = (int)(j % p->nbuf);
@@ -697,6 +743,17 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->G = (c.H > 256 && (c.H % 128) == 0 && (c.B % 16) == 0) ? std::max(1, std::min(4, Gw)) : 1;
         p->D = c.inflight ? c.inflight : std::max(1, std::min(2 * p->G, ncu / bcu - 1));
         p->P = c.prod_streams ? c.prod_streams : (c.H > 256 ? 2 : 1);
+        // With the one-launch recurrence (H > 256, asr::rnn_recur_persist_launch)
+        // production holds its CUs for ~5 us a frame instead of ~14 beside
+        // the GEMMs, so three decodes run at once where each production
+        // stream keeps the recurrence's workgroups (C5, 10 / 3 steps: D = 2 /
+        // 3 / 4 3.45 / 4.24 / 4.27 M frames/s; P = 3 leaves too few CUs per
+        // stream and falls back to the per-frame steps: 1.7-2.1 M; run sv).
+        if (!c.inflight && p->G == 1 && c.H > 256 && (c.H % 128) == 0 && c.H >= 384 && c.H <= 1024 &&
+            c.B <= 256) {
+            const int nwg = (c.H / 32) * ((c.B + 15) / 16);
+            if ((ncu - 3 * bcu) / std::max(1, p->P) >= nwg && 4 * bcu <= ncu) p->D = 3;
+        }
     } else {   // chip-filling batches otherwise (C3's beam 100, BL's H = 2048): one decode at a time
         p->mode = SHARED;
         p->dcus = c.decode_cus > 0 ? std::min(c.decode_cus, ncu - 8) : 0;
@@ -726,6 +783,13 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     if (p->fuse && p->mode == SHARED) {
         const int S = c.segments ? c.segments : auto_segments(c, kcap);
         p->S = std::max(1, std::min(S, c.T));
+    }
+    // H > 256 small batches with the wide decoder (C5): the production hands
+    // the decode two T-segments (the first decode starts after half of the
+    // first production, the last batch's drain is half a decode)
+    if (p->mode == GROUPS2 && p->G == 1 && c.V + 1 > 64 && c.V <= 4096) {
+        const int S = c.segments ? c.segments : 2;
+        p->S = std::max(1, std::min(S, c.T / 2));
     }
     // fragment-major P between the input projection and the split-bf16 fused
     // recurrence (measured against row-major P: production ~2-3 % shorter,
@@ -787,12 +851,16 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         // at C4, D = 2, profiles/r04/bench_scan.md)
         for (int d = 0; d < p->D; d++) mkr(ASR_PIPE_ROLE_DECODE, &p->s_dec[d], 0, p->dcus ? p->dcus : ncu);
         for (int q = 0; q < p->P; q++) mkr(ASR_PIPE_ROLE_PRODUCTION, &p->s_prod[q], p->dcus, ncu);
+        p->pcus = (ncu - p->dcus) / std::max(1, p->P);
         if (p->grows > 0) mkr(ASR_PIPE_ROLE_DECODE_CU_GEMM, &p->s_gdec, 0, p->dcus);
     } else {
         for (int d = 0; d < p->D; d++)
             mkr(ASR_PIPE_ROLE_DECODE, &p->s_dec[d], p->gcu ? (d % p->ngroups) * p->gcu : 0,
                 p->gcu ? (d % p->ngroups + 1) * p->gcu : ncu);
         for (int q = 0; q < p->P; q++) mkr(ASR_PIPE_ROLE_PRODUCTION, &p->s_prod[q], p->gcu ? p->ngroups * p->gcu : 0, ncu);
+        // each production stream's share of its CUs, for a recurrence whose
+        // workgroups must all be resident at once (P of them may run together)
+        p->pcus = (ncu - (p->gcu ? p->ngroups * p->gcu : 0)) / std::max(1, p->P);
         if (p->split) mkr(ASR_PIPE_ROLE_GEMM, &p->s_gemm, 0, ncu);   // the GEMMs on every CU
         if (p->tail_own) mkr(ASR_PIPE_ROLE_GEMM, &p->s_tail, 0, ncu);
         else p->s_tail = p->s_gemm;

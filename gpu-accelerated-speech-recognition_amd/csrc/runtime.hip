@@ -21,6 +21,7 @@ thread_local std::string g_last_error;
 
 thread_local int asr_internal_rnn_kind = -1;
 thread_local int asr_internal_graph_now = 0;
+thread_local int asr_internal_persist_cus = 0;
 thread_local int asr_internal_gemm_tiled = 0;
 
 void asr_internal_set_error(const char* what, const char* msg, const char* file, int line) {
@@ -298,6 +299,9 @@ static int rnn_recurrence(const float* h0, const float* W_hh, const float* b_ih,
         if (rnn_use_mfma(B, H)) return asr::rnn_recur_mfma_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
         return asr::rnn_recur_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, st);
     }
+    // one launch for all T frames where every workgroup fits beside the rest
+    const int rc = asr::rnn_recur_persist_launch(h0, W_hh, b_ih, b_hh, hid, T, B, H, asr_internal_persist_cus, st);
+    if (rc != ASR_ERR_UNSUPPORTED) return rc;
     return rnn_recurrence_frames(h0, W_hh, b_ih, b_hh, &hid, 1, T, B, H, st);
 }
 
@@ -518,6 +522,7 @@ struct asr_ctc {
     int cap_len = 0;
     // segmented decode (asr_ctc_decode_segment)
     int seg_next = 0;                // first frame of the next segment (0: none in progress)
+    int seg_waves = 0;               // the segmented decode's kernel (one-wave list kernel or wide)
     int seg_T = 0, seg_B = 0, seg_is_log = 0;
     long seg_fs = 0, seg_us = 0;
     unsigned char* d_seg = nullptr;  // [B][seg_bytes] saved beams
@@ -865,10 +870,10 @@ int decode_frames(asr_ctc* h, const float* d_emis, int T, int B, long frame_stri
         h->args.emis = d_emis;
         h->args.t0 = t0;
         h->args.t1 = t1;
-        rc = launch_decode_events(h, ASR_CTC_WAVES_LIST, st, true);
+        rc = launch_decode_events(h, h->seg_waves, st, true);
         if (rc) return rc;
         if (t1 < T) return ASR_OK;
-        return finish_decode(h, st, B, T, ASR_CTC_WAVES_LIST);
+        return finish_decode(h, st, B, T, h->seg_waves);
     }
     rc = ensure_ws(h, B, T);
     if (rc) return rc;
@@ -892,7 +897,9 @@ int decode_frames(asr_ctc* h, const float* d_emis, int T, int B, long frame_stri
     const long Beff = std::min<long>((long)B * h->concurrency, 1L << 30);
     int waves = valid_waves(h, h->waves_override && !h->cu_mode ? h->waves_override : auto_waves(h, (int)Beff));
     if (h->ts && waves < 0) waves = valid_waves(h, 8);
-    if (segmented) waves = ASR_CTC_WAVES_LIST;   // checked by the caller
+    // segmented: the one-wave kernel, or the wide one for V > 63 (checked by the caller)
+    if (segmented) waves = h->V + 1 > 64 ? 8 : ASR_CTC_WAVES_LIST;
+    h->seg_waves = waves;
     asr::CtcArgs& a = h->args;
     a.g = plan(h, waves);
     a.emis = d_emis;
@@ -919,7 +926,8 @@ int decode_frames(asr_ctc* h, const float* d_emis, int T, int B, long frame_stri
     a.seg_state = nullptr;
     a.seg_bytes = 0;
     if (segmented) {
-        const size_t sb = asr::ctc_seg_bytes_wave(a.g), need = sb * (size_t)B;
+        const size_t sb = waves < 0 ? asr::ctc_seg_bytes_wave(a.g) : asr::ctc_seg_bytes_wide(asr::ctc_row_capacity(a.g.kcap));
+        const size_t need = sb * (size_t)B;
         if (h->cap_seg < need) {
             hipStreamSynchronize(st);
             hipFree(h->d_seg);
@@ -1031,9 +1039,10 @@ int asr_ctc_decode_segment(asr_ctc_t* h, const float* d_emis, int T, int t0, int
         if (h_lengths)
             for (int b = 0; b < B; b++)
                 if (h_lengths[b] < 0 || h_lengths[b] > T) return ASR_ERR_ARG;
-        // the one-wave kernel carries the beam across segments: V <= 63, CPU
-        // semantics, no timesteps
-        if (h->ts || h->cu_mode || !asr::ctc_wave_supported(plan(h, ASR_CTC_WAVES_LIST), 0))
+        // the one-wave kernel (V <= 63) or the wide kernel (V > 63) carries
+        // the beam across segments: CPU semantics, no timesteps
+        const bool wide = h->V + 1 > 64 && h->V <= asr::WIDE_VMAX;
+        if (h->ts || h->cu_mode || (!wide && !asr::ctc_wave_supported(plan(h, ASR_CTC_WAVES_LIST), 0)))
             return ASR_ERR_UNSUPPORTED;
     }
     const int rc = decode_frames(h, d_emis, T, B, frame_stride, utt_stride, t0 == 0 ? h_lengths : nullptr,

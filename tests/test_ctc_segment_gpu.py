@@ -26,7 +26,8 @@ def _segmented(d_em, T, B, V, beam, cuts, is_log, lengths=None, fs=None, us=None
                          frame_stride=fs, utt_stride=us)
     beams = d.beams(max_hyps=d.config()[0])
     lab, lp = d.best()
-    assert d.config()[1] == asr.ASR_CTC_WAVES_LIST
+    # the one-wave kernel carries the beam for V <= 63, the wide kernel (8 waves) above
+    assert d.config()[1] == (asr.ASR_CTC_WAVES_LIST if V + 1 <= 64 else 8)
     d.close()
     return beams, lab, lp
 
@@ -67,6 +68,27 @@ def test_segmented_equals_whole(T, B, V, beam, cuts, sigma):
     sub = list(range(0, B, max(1, B // 4)))[:4]
     ref = oracle.decode(np.ascontiguousarray(emis[:, sub, :]), beam, 0, nthreads=cpu_threads(), max_hyps=256)
     assert_beams_equal([seg[0][u] for u in sub], ref, f"segmented vs oracle, cuts {cuts}")
+
+
+@pytest.mark.parametrize("T,B,V,beam,cuts,sigma,lengths", [
+    (60, 6, 100, 20, [20, 40], 3.0, None),
+    (48, 5, 1000, 200, [1, 24, 47], 2.0, None),          # C5's vocabulary and beam, one-frame segments
+    (50, 7, 300, 40, [25], 1.0, [50, 25, 24, 26, 0, 1, 49]),   # lengths ending at / around the cut
+])
+def test_segmented_wide_equals_whole(T, B, V, beam, cuts, sigma, lengths):
+    """V > 63: the wide kernel (8 waves per utterance, vocabulary tiles, the
+    first tile of each frame precomputed per segment) carries its beam across
+    segments too — the C5 pipeline hands the decode two T-segments.  Bit-
+    identical to the whole decode, which is the oracle's on a subset."""
+    emis = oracle.synthetic_emissions(T, B, V, seed0=919 + V, sigma=sigma)
+    d_em = asr.DeviceMatrix.from_numpy(emis.reshape(T * B, V))
+    seg = _segmented(d_em, T, B, V, beam, cuts, False, lengths=lengths)
+    whole = _whole(d_em, T, B, V, beam, False, lengths=lengths, waves=0)
+    _same(seg, whole, f"wide, cuts {cuts}")
+    if V <= 300 and lengths is None:
+        sub = [0, B - 1]
+        ref = oracle.decode(np.ascontiguousarray(emis[:, sub, :]), beam, 0, nthreads=2, max_hyps=256)
+        assert_beams_equal([seg[0][u] for u in sub], ref, f"wide segmented vs oracle, cuts {cuts}")
 
 
 def test_segmented_with_lengths_and_strides():

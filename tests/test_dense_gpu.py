@@ -397,6 +397,7 @@ def test_rnn_step_tilings_same_bits(T, B, H, monkeypatch):
     (ASR_RNN_STEP_NT; the automatic choice follows the shape: BL's 256 x
     2048 takes 4) gives the same bits, and agrees with torch fp32."""
     monkeypatch.setenv("ASR_RNN_GRAPH", "0")   # a captured graph would keep the first tiling
+    monkeypatch.setenv("ASR_RNN_PERSIST", "0")   # the per-frame step launches (the one-launch form: below)
     rng = np.random.default_rng(T + B + H)
     I = 32
     x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
@@ -415,6 +416,38 @@ def test_rnn_step_tilings_same_bits(T, B, H, monkeypatch):
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])
     close(outs[0], _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh), 1e-4)
+
+
+@pytest.mark.parametrize("T,B,H,with_h0", [(40, 32, 1024, False), (25, 37, 512, True), (12, 100, 384, False),
+                                             (9, 64, 1024, True), (500, 32, 1024, False), (3, 5, 640, True)])
+def test_rnn_persistent_recurrence_same_bits(T, B, H, with_h0, monkeypatch):
+    """H > 256 in ONE launch (each workgroup's W_hh slice in registers for all
+    T frames, h_t handed between workgroups through memory with write-through
+    stores, a step counter and coherent loads): the same bits as the T
+    per-frame step launches (ASR_RNN_PERSIST=0), with and without h0, ragged
+    batches, C5's 32 x 1024 over 500 frames; and torch fp32 agrees."""
+    monkeypatch.setenv("ASR_RNN_GRAPH", "0")
+    rng = np.random.default_rng(T * 7 + B + H)
+    I = 48
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    w_ih = rng.uniform(-s, s, (I, H)).astype(np.float32)
+    w_hh = rng.uniform(-s, s, (H, H)).astype(np.float32)
+    b_ih = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    b_hh = rng.uniform(-0.1, 0.1, H).astype(np.float32)
+    h0 = rng.uniform(-1, 1, (B, H)).astype(np.float32) if with_h0 else None
+    W = [dm(w_ih), dm(w_hh), dm(b_ih.reshape(H, 1)), dm(b_hh.reshape(H, 1))]
+    dx = dm(x)
+    outs = []
+    for persist in ("0", "1", "1"):
+        monkeypatch.setenv("ASR_RNN_PERSIST", persist)
+        hid = asr.DeviceMatrix(T * B, H)
+        asr.rnn_fwd(dx, *W, hid, T, B, h0=dm(h0) if with_h0 else None)
+        outs.append(hid.toCpu())
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    if T <= 40:
+        close(outs[0], _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
 
 
 def test_rnn_multilayer():

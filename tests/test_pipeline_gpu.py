@@ -44,6 +44,8 @@ def _sequential(x, W, T, B, inp, H, V, beam, recur, fused=False):
     (30, 300, 32, 64, 29, 100, "chip-filling batches", asr.RNN_RECUR_MFMA),  # beam 100 (C3-like): fused
     (12, 300, 32, 384, 47, 60, "chip-filling batches", asr.RNN_RECUR_AUTO),  # H > 256 (BL-like)
     (20, 8, 32, 384, 29, 8, "CU groups (H > 256)", asr.RNN_RECUR_AUTO),
+    # H > 256 with the wide decoder (C5-like): two T-segments, the one-launch recurrence
+    (24, 16, 32, 384, 100, 12, "CU groups (H > 256)", asr.RNN_RECUR_AUTO),
 ])
 def test_pipeline_matches_sequential(T, B, inp, H, V, beam, mode, recur):
     W = _weights(inp, H, V, seed=T + B + H)
