@@ -243,8 +243,10 @@ int asr_ctc_decode_ex(asr_ctc_t* h, const float* d_emis, int T, int B, long fram
  * segment is d_emis[(t - t0)*frame_stride + b*utt_stride + v].  T, B, the
  * strides and is_log must be the same for every segment.  Results are
  * bit-identical to a whole decode of the same frames.  Runs the one-wave
- * kernel (ASR_CTC_WAVES_LIST): V <= 63, CPU semantics, timesteps off, else
- * ASR_ERR_UNSUPPORTED; ASR_ERR_STATE for a segment out of order.  Overflow
+ * kernel (ASR_CTC_WAVES_LIST) for V <= 63 and the large-vocabulary kernel
+ * for 63 < V <= 4096 (each frame's first vocabulary tile precomputed per
+ * segment); CPU semantics and timesteps off, else ASR_ERR_UNSUPPORTED;
+ * ASR_ERR_STATE for a segment out of order.  Overflow
  * retry (automatic capacity): asr_ctc_get_best re-decodes the whole batch
  * from the FIRST segment's d_emis over T frames, so that pointer must then
  * address all T frames (e.g. segments of one [T][B][V] buffer); a caller

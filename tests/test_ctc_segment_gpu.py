@@ -144,9 +144,10 @@ def test_segment_errors():
             d.decode_segment(d_em.ptr, T, 0, 10, B, False)
         assert e.value.status == asr.ASR_ERR_UNSUPPORTED
         d.close()
-    Vw = 100   # the large-vocabulary kernel keeps whole decodes
+    Vw = 100   # the large-vocabulary kernel segments too (round 5), in CPU semantics only
     ew = asr.DeviceMatrix.from_numpy(oracle.synthetic_emissions(T, B, Vw, seed0=6).reshape(T * B, Vw))
     d = asr.CTCDecoder(Vw, beam, 0)
+    d.set_semantics(asr.SEMANTICS_CUDA)
     with pytest.raises(asr.AsrError) as e:
         d.decode_segment(ew.ptr, T, 0, 10, B, False)
     assert e.value.status == asr.ASR_ERR_UNSUPPORTED
