@@ -11,6 +11,8 @@
 // ============================================================================
 #include "dense.h"
 
+#include <cstring>
+
 namespace asr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1155,7 +1157,6 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 // chunk order (4 MFMAs per 16-k chunk, k = 16 i + 4 g + j), the 8 partials
 // summed in wave order, tanhf((P_t + hh) + (b_hh + b_ih)); frame 0 without
 // h0 is bias_tanh's tanhf(P_0 + (b_hh + b_ih)).
-__device__ int g_rnn_persist_timeout = 0;
 constexpr int RP_LDS = 96 * 1024;   // one workgroup per CU
 constexpr int RP_SC1 = 16;          // buffer-instruction cache policy: sc1 (write-through / coherent)
 
@@ -1165,7 +1166,7 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
                                                                           const float* __restrict__ b_ih,
                                                                           const float* __restrict__ b_hh,
                                                                           float* hid, int T, int B, int H,
-                                                                          unsigned* ctr) {
+                                                                          unsigned* ctr, int* timeout_flag) {
     extern __shared__ __attribute__((aligned(16))) f32x4 rp_part[];   // [RSM_WAVES][RB * NT][64], then the abort flag
     int& rp_abort = *reinterpret_cast<int*>(rp_part + RSM_WAVES * RB * NT * 64);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1198,7 +1199,7 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
                     __builtin_amdgcn_s_sleep(2);
                     if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s at 100 MHz
                         rp_abort = 1;
-                        __hip_atomic_store(&g_rnn_persist_timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(timeout_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         break;
                     }
                 }
@@ -1268,13 +1269,35 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
     }
 }
 
+// The timeout flag in pinned, device-mapped host memory: the host reads it
+// with no HIP call (a synchronous copy would wait for every stream's work).
+static int* persist_flag_host = nullptr;
+static int* persist_flag_dev = nullptr;
+static int persist_flag(int** dev) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!persist_flag_host) {
+        void* h = nullptr;
+        ASR_HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(h, 0, 64);
+        void* d = nullptr;
+        ASR_HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
+        persist_flag_host = static_cast<int*>(h);
+        persist_flag_dev = static_cast<int*>(d);
+    }
+    *dev = persist_flag_dev;
+    return ASR_OK;
+}
+
 template <int RB, int NT, int KCH>
 static int launch_persist(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
                           int T, int B, int H, unsigned* ctr, hipStream_t s) {
     static AsrAttrOnce attr;
     if (int r_ = attr.set((const void*)rnn_recur_persist_kernel<RB, NT, KCH>, RP_LDS)) return r_;
+    int* flag = nullptr;
+    if (int r_ = persist_flag(&flag)) return r_;
     hipLaunchKernelGGL((rnn_recur_persist_kernel<RB, NT, KCH>), dim3((unsigned)(H / (16 * NT)), (unsigned)((B + 16 * RB - 1) / (16 * RB))),
-                       dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh, b_ih, b_hh, hid, T, B, H, ctr);
+                       dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, flag);
     ASR_LAUNCH_TRY();
     return ASR_OK;
 }
@@ -1331,9 +1354,7 @@ int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_i
 }
 
 int rnn_persist_status(int* timed_out) {
-    int v = 0;
-    ASR_HIP_TRY(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_rnn_persist_timeout), sizeof(int)));
-    *timed_out = v;
+    *timed_out = persist_flag_host ? __atomic_load_n(persist_flag_host, __ATOMIC_ACQUIRE) : 0;
     return ASR_OK;
 }
 
