@@ -1334,11 +1334,21 @@ int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_i
         (h0 && ((uintptr_t)h0 % 16) != 0) || (long)B * H * 4 >= 0x7fffffffL)
         return ASR_ERR_UNSUPPORTED;
     const int nwg = (H / 32) * ((B + 15) / 16);
-    if (cus <= 0) {   // no hint: half of the device's CUs (room beside it)
+    if (cus <= 0) {   // no hint: half of the CUs the stream's mask allows (room beside it)
         int dev = 0, ncu = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return ASR_ERR_UNSUPPORTED;
-        cus = ncu / 2;
+        int avail = ncu;
+        if (s) {   // a caller's CU-masked stream
+            uint32_t m[32] = {};
+            const int words = std::min(32, (ncu + 31) / 32);
+            if (hipExtStreamGetCUMask(s, (uint32_t)words, m) == hipSuccess) {
+                int n = 0;
+                for (int i = 0; i < words; i++) n += __builtin_popcount(m[i]);
+                if (n > 0) avail = std::min(avail, n);
+            }
+        }
+        cus = avail / 2;
     }
     if (nwg > cus) return ASR_ERR_UNSUPPORTED;   // every workgroup resident at once
     unsigned* ctr = nullptr;

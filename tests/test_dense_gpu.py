@@ -450,6 +450,30 @@ def test_rnn_persistent_recurrence_same_bits(T, B, H, with_h0, monkeypatch):
         close(outs[0], _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
 
 
+def test_rnn_persistent_recurrence_on_a_masked_stream(monkeypatch):
+    """A caller's CU-masked stream with fewer CUs than the one-launch
+    recurrence has workgroups (C5's 64 on a 32-CU stream): the launcher reads
+    the stream's mask and takes the per-frame steps instead (a launch whose
+    workgroups cannot all be resident would wait for them); same bits."""
+    import bench
+    monkeypatch.setenv("ASR_RNN_GRAPH", "0")
+    T, B, I, H = 30, 32, 64, 1024
+    rng = np.random.default_rng(31)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    W = [dm(rng.uniform(-s, s, (I, H)).astype(np.float32)), dm(rng.uniform(-s, s, (H, H)).astype(np.float32)),
+         dm(rng.uniform(-0.1, 0.1, (H, 1)).astype(np.float32)), dm(rng.uniform(-0.1, 0.1, (H, 1)).astype(np.float32))]
+    dx = dm(x)
+    ref = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dx, *W, ref, T, B)
+    st = bench.cu_range_stream(0, 32)
+    got = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dx, *W, got, T, B, stream=st.cuda_stream)
+    st.synchronize()
+    assert np.array_equal(got.toCpu(), ref.toCpu())
+    bench.destroy_raw_streams()
+
+
 def test_rnn_multilayer():
     """num_layers > 1 (RNN.h:13-20): layer l+1 consumes layer l's hiddens."""
     T, B, I, H, L = 15, 6, 40, 64, 3
