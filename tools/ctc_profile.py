@@ -101,8 +101,12 @@ def run(T, B, V, beam, sigma, waves, reps, stamps, wstamps=False):
         out["cycles_per_step"] = {PH[i]: round(per[i], 1) for i in range(13)
                                   if PH[i] != "-" and not PH[i].startswith("n:")}
         out["events_per_frame"] = {PH[i][2:]: round(per[i], 2) for i in range(13) if PH[i].startswith("n:")}
+        if PH is WIDE_PHASES:   # slot 9: window keys | (row, column) pairs listed << 32
+            out["events_per_frame"]["keys in stage-1 window"] = round(float((buf[:, 9] & 0xFFFFFFFF).mean()) / T, 2)
+            out["events_per_frame"]["pairs listed"] = round(float((buf[:, 9] >> 32).mean()) / T, 2)
         ranks = (buf[:, 15] & 0xFFFFFFFF).astype(np.float64)
-        out["per_frame"] = {"fallbacks": round(per[13], 4), "exact_passes": round(per[14], 3),
+        out["per_frame"] = {("stage1_passes" if PH is WIDE_PHASES else "fallbacks"): round(per[13], 4),
+                            "exact_passes": round(per[14], 3),
                             "ranks": round(ranks.mean() / T, 3),
                             "mean_cd": round(float((buf[:, 15] >> 32).sum() / max(1.0, ranks.sum())), 2)}
         out["cycles_total"] = round(per[:7].sum() + (per[8] if PH is WIDE_PHASES else 0.0), 1)
