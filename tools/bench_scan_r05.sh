@@ -16,4 +16,7 @@ python tools/bench_scan.py profiles/r05/bench_scan.md \
   "sn:GPU_MAX_HW_QUEUES 4 / 8 / 16 / 24 / 32 (queue fit: production streams first)" \
   "sn2:4 / 8 / 16 queues, queue fit: the larger of D / P first" \
   "so:4 / 8 / 16 queues, queue fit: production streams down to half the decodes, then both (the product)" \
+  "c5n:C5 and BL after the wide decoder's superset-test candidates (13.2 us per frame)" \
+  "c5s:C5 T-segments 2 / 3 / 4 (13.2 us decoder)" \
+  "fin_r5c:final tree (12.3 us wide decoder): C4, C2 with parity witness; C5, BL" \
   "$@"
