@@ -1188,9 +1188,34 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
     if (tid == 0) rp_abort = 0;
     const long slab = (long)B * H;
     const int sbytes = (int)(slab * 4);
+    // this thread's outputs (EPT per step): their byte offset in a frame and
+    // (b_hh + b_ih), loaded once
+    constexpr int EPT = RB * NT * 256 / (64 * RSM_WAVES);
+    static_assert(EPT * 64 * RSM_WAVES == RB * NT * 256, "outputs per thread");
+    int eoff[EPT], etl[EPT], el[EPT], ej[EPT];
+    float ebias[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; k++) {
+        const int e = tid + k * 64 * RSM_WAVES;
+        const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
+        const int rb = tl / NT, nt = tl - rb * NT;
+        const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
+        eoff[k] = (r * H + n) * 4;   // rows past B: past the resource (load 0, store dropped)
+        etl[k] = tl;
+        el[k] = l;
+        ej[k] = j;
+        ebias[k] = b_hh[n] + b_ih[n];
+    }
     for (int t = 0; t < T; t++) {
         float* ht = hid + (long)t * slab;
         const float* hp = t > 0 ? hid + (long)(t - 1) * slab : h0;
+        // P_t (the input projection, in place in h_t) does not depend on
+        // h_{t-1}: loaded before the wait for frame t - 1
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(ht, (short)0, sbytes, 0x00020000);
+        float Pv[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; k++)
+            Pv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_t, eoff[k], 0, RP_SC1));
         if (t > 0) {   // every workgroup has published frame t - 1
             if (tid == 0) {
                 const unsigned target = nwg * (unsigned)t;
@@ -1207,7 +1232,6 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
             __syncthreads();
             if (rp_abort) return;
         }
-        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(ht, (short)0, sbytes, 0x00020000);
         if (hp) {
             const auto rs_p = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hp), (short)0, sbytes, 0x00020000);
             f32x4 acc[RB][NT];
@@ -1239,27 +1263,20 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
 #pragma unroll
                 for (int nt = 0; nt < NT; nt++) rp_part[(w * RB * NT + rb * NT + nt) * 64 + lane] = acc[rb][nt];
             __syncthreads();
-            for (int e = tid; e < RB * NT * 256; e += 64 * RSM_WAVES) {
-                const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
-                const int rb = tl / NT, nt = tl - rb * NT;
-                const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
+#pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                const int tl = etl[k], l = el[k], j = ej[k];
                 float hh = rp_part[tl * 64 + l][j];
 #pragma unroll
                 for (int q = 1; q < RSM_WAVES; q++) hh += rp_part[(q * RB * NT + tl) * 64 + l][j];
-                const int off = (r * H + n) * 4;   // rows past B: past the resource (load 0, store dropped)
-                const float P = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_t, off, 0, RP_SC1));
-                const float y = tanhf((P + hh) + (b_hh[n] + b_ih[n]));
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, off, 0, RP_SC1);
+                const float y = tanhf((Pv[k] + hh) + ebias[k]);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, eoff[k], 0, RP_SC1);
             }
         } else {   // h_{-1} = 0: bias_tanh's formula
-            for (int e = tid; e < RB * NT * 256; e += 64 * RSM_WAVES) {
-                const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
-                const int rb = tl / NT, nt = tl - rb * NT;
-                const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
-                const int off = (r * H + n) * 4;
-                const float P = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_t, off, 0, RP_SC1));
-                const float y = tanhf(P + (b_hh[n] + b_ih[n]));
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, off, 0, RP_SC1);
+#pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                const float y = tanhf(Pv[k] + ebias[k]);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, eoff[k], 0, RP_SC1);
             }
         }
         // publish frame t: every wave's stores drained, then one add per workgroup
