@@ -1148,7 +1148,10 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 //     h_{t-1} (and of P_t) is a buffer load with the sc1 bit (not served
 //     from this CU's L1) — the hand-off form of cdna_hip_programming.md §6
 //     Guideline 16 (one workgroup per CU: the launch requests more than half
-//     of a CU's LDS).
+//     of a CU's LDS);
+//   * P_t does not depend on h_{t-1}: each thread loads its P_t before the
+//     wait, so that load is off the step's critical path (C5 production
+//     20.0 -> 18.5 ms per batch).
 // Every workgroup must be resident at once: the launcher only takes grids of
 // at most `cus` workgroups (the CUs the caller's stream may use), and a
 // bounded spin (0.5 s without progress) ends the kernel with an error flag
