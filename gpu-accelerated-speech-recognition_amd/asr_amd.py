@@ -50,7 +50,7 @@ EXPORTS = [
     "asr_host_free", "asr_memcpy_h2d", "asr_memcpy_d2h", "asr_memcpy_d2d", "asr_memset",
     "asr_stream_create", "asr_stream_destroy", "asr_stream_sync", "asr_device_sync",
     "asr_matmul", "asr_matmul_ta", "asr_matmul_tb", "asr_matadd", "asr_linear_fwd",
-    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_recur_fwd", "asr_rnn_emit_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
+    "asr_rnn_cell_fwd", "asr_rnn_fwd", "asr_rnn_recur_fwd", "asr_rnn_persist_stats", "asr_rnn_emit_fwd", "asr_rnn_bidir_workspace_bytes", "asr_rnn_bidir_fwd",
     "asr_ctc_create", "asr_ctc_destroy", "asr_ctc_decode",
     "asr_ctc_get_best", "asr_ctc_get_beams", "asr_ctc_last_kernel_ms", "asr_ctc_set_waves",
     "asr_ctc_get_config", "asr_ctc_decode_ex", "asr_ctc_decode_segment", "asr_ctc_set_semantics",
@@ -117,6 +117,7 @@ def lib() -> ctypes.CDLL:
         "asr_rnn_cell_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
         "asr_rnn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_rnn_recur_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp],
+        "asr_rnn_persist_stats": [ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)],
         "asr_rnn_set_recurrence": [_i],
         "asr_rnn_get_recurrence": [ctypes.POINTER(_i)],
         "asr_set_dense_arith": [_i],
@@ -279,6 +280,15 @@ def rnn_recur_fwd(W_hh: DeviceMatrix, b_ih: DeviceMatrix, b_hh: DeviceMatrix, hi
     check(lib().asr_rnn_recur_fwd(h0.ptr if h0 else None, W_hh.ptr, b_ih.ptr, b_hh.ptr, hid.ptr,
                                   T, B, H, stream), "asr_rnn_recur_fwd")
     return hid
+
+
+def rnn_persist_stats() -> tuple:
+    """(launches, recoveries) of the one-launch H > 256 recurrence in this
+    process (asr_rnn_persist_stats): recoveries are launches that gave up
+    waiting for their workgroups and were finished by the recovery kernel."""
+    n, r = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    check(lib().asr_rnn_persist_stats(ctypes.byref(n), ctypes.byref(r)), "asr_rnn_persist_stats")
+    return n.value, r.value
 
 
 def rnn_emit_fwd(W_hh: DeviceMatrix, b_ih: DeviceMatrix, b_hh: DeviceMatrix, W_out: DeviceMatrix,

@@ -48,11 +48,16 @@ int rnn_step_mfma_launch(float* ht, const float* hp, const float* Whh, const flo
 // workgroups handing h_t to each other in memory (same bits as the step
 // launches); ASR_ERR_UNSUPPORTED outside 384 <= H <= 1024, H % 128 == 0,
 // B <= 256, or when its (H / 32) x ceil(B / 16) workgroups exceed `cus`
-// (the CUs the caller's stream gives this launch; <= 0: half of the device).
+// (the CUs the caller's stream gives this launch; <= 0: half of the device's
+// CUs less those of other such launches in flight), or while the stream is
+// capturing.  Fail-safe: a launch whose workgroups are not all resident gives
+// up after 0.5 s without progress and a recovery kernel on the same stream
+// finishes its frames with the same bits.
 int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
                              int T, int B, int H, int cus, hipStream_t s);
-// 1 when a persistent recurrence gave up waiting (0.5 s without progress).
-int rnn_persist_status(int* timed_out);
+// Process-wide counts of one-launch recurrences and of those that completed
+// through the recovery kernel (counted once their stream passed them).
+int rnn_persist_stats(long long* launches, long long* recoveries);
 constexpr int STEP_MAXB = 4;
 // The same step for nb <= STEP_MAXB batches of B rows at once (one launch; batch j:
 // h_t at hts[j], h_{t-1} at hps[j]); nb > 1 needs B % 16 == 0.  Same bits.

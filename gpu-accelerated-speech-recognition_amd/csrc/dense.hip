@@ -11,7 +11,9 @@
 // ============================================================================
 #include "dense.h"
 
+#include <cstddef>
 #include <cstring>
+#include <vector>
 
 namespace asr {
 
@@ -1140,8 +1142,9 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 // each other through memory inside the launch:
 //   * h_t is stored write-through (buffer stores with the sc1 bit) into hid
 //     (its final place); every storing wave drains its stores (vmcnt(0)),
-//     the workgroup barriers, and one lane adds 1 to a step counter
-//     (agent-scope atomic);
+//     the workgroup barriers, and one lane records the frames it published
+//     (prog[wg]) and adds 1 to the launch's step counter (agent-scope
+//     atomic);
 //   * before frame t a workgroup's first lane polls the counter (agent-scope
 //     relaxed loads, s_sleep between) until all nWG workgroups have
 //     published frame t - 1, the workgroup barriers, and every load of
@@ -1152,89 +1155,92 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 //   * P_t does not depend on h_{t-1}: each thread loads its P_t before the
 //     wait, so that load is off the step's critical path (C5 production
 //     20.0 -> 18.5 ms per batch).
-// Every workgroup must be resident at once: the launcher only takes grids of
-// at most `cus` workgroups (the CUs the caller's stream may use), and a
-// bounded spin (0.5 s without progress) ends the kernel with an error flag
-// (asr::rnn_persist_status) instead of hanging.
+// Every workgroup must be resident at once.  The launcher only takes grids
+// of at most `cus` workgroups (the CUs the caller's stream may use), but
+// residency is not guaranteed (other work on the same CUs, another process,
+// a one-launch recurrence of another stream), so the launch is fail-safe:
+//   * a wait without progress for 0.5 s sets the launch's abort word, and
+//     every workgroup that sees it (waiting, or dispatched late) exits;
+//   * a one-workgroup recovery kernel follows on the stream: it exits at
+//     once unless the abort word is set, and then computes every frame a
+//     tile had not published (prog[wg], which differs by at most one frame
+//     between workgroups) with the same arithmetic, so the call's bits are
+//     those of an undisturbed launch (slower, never wrong);
+//   * each launch owns its control block (counter, abort word, prog[]) until
+//     an event recorded after its recovery kernel has completed.
 // The arithmetic per output is the step kernel's: each wave's K slice in
 // chunk order (4 MFMAs per 16-k chunk, k = 16 i + 4 g + j), the 8 partials
 // summed in wave order, tanhf((P_t + hh) + (b_hh + b_ih)); frame 0 without
 // h0 is bias_tanh's tanhf(P_0 + (b_hh + b_ih)).
 constexpr int RP_LDS = 96 * 1024;   // one workgroup per CU
 constexpr int RP_SC1 = 16;          // buffer-instruction cache policy: sc1 (write-through / coherent)
+constexpr int RP_MAXWG = (1024 / 32) * (256 / 16);        // H <= 1024 (NT = 2), B <= 256
+constexpr unsigned long long RP_TIMEOUT = 50000000ull;   // 0.5 s of s_memrealtime (100 MHz)
 
+// One launch's control block (device memory; the head is zeroed on the
+// stream before the launch).
+struct PersistCtl {
+    unsigned ctr;              // publications: one per workgroup and frame
+    unsigned abort;            // 1: a workgroup gave up waiting
+    unsigned pad[14];
+    unsigned prog[RP_MAXWG];   // frames published, per workgroup
+};
+
+// This thread's share of one tile: its W_hh slice, A-row offsets and
+// output slots (the same for every frame).
 template <int RB, int NT, int KCH>
-__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const float* h0,
-                                                                          const float* __restrict__ Whh,
-                                                                          const float* __restrict__ b_ih,
-                                                                          const float* __restrict__ b_hh,
-                                                                          float* hid, int T, int B, int H,
-                                                                          unsigned* ctr, int* timeout_flag) {
-    extern __shared__ __attribute__((aligned(16))) f32x4 rp_part[];   // [RSM_WAVES][RB * NT][64], then the abort flag
-    int& rp_abort = *reinterpret_cast<int*>(rp_part + RSM_WAVES * RB * NT * 64);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int g = lane >> 4, c = lane & 15;
-    const int n0 = blockIdx.x * (16 * NT), r0 = blockIdx.y * (16 * RB);
-    const unsigned nwg = gridDim.x * gridDim.y;
-    const int kbeg = w * (H / RSM_WAVES);
-    // this wave's W_hh slice: chunk i, tile nt, MFMA j -> W[kbeg + 16 i + 4 g + j][n0 + 16 nt + c]
-    float bw[KCH][NT][4];
-#pragma unroll
-    for (int i = 0; i < KCH; i++)
-#pragma unroll
-        for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) bw[i][nt][j] = Whh[(long)(kbeg + 16 * i + 4 * g + j) * H + n0 + 16 * nt + c];
-    int arow[RB];   // row offsets (floats) of this lane's A rows: rows past B read row B - 1 (never stored)
-#pragma unroll
-    for (int rb = 0; rb < RB; rb++) arow[rb] = min(r0 + rb * 16 + c, B - 1) * H + kbeg + 4 * g;
-    if (tid == 0) rp_abort = 0;
-    const long slab = (long)B * H;
-    const int sbytes = (int)(slab * 4);
-    // this thread's outputs (EPT per step): their byte offset in a frame and
-    // (b_hh + b_ih), loaded once
-    constexpr int EPT = RB * NT * 256 / (64 * RSM_WAVES);
+struct RpTile {
+    static constexpr int EPT = RB * NT * 256 / (64 * RSM_WAVES);   // outputs per thread
     static_assert(EPT * 64 * RSM_WAVES == RB * NT * 256, "outputs per thread");
+    float bw[KCH][NT][4];
+    int arow[RB];
     int eoff[EPT], etl[EPT], el[EPT], ej[EPT];
     float ebias[EPT];
+
+    __device__ __forceinline__ void setup(const float* __restrict__ Whh, const float* __restrict__ b_ih,
+                                          const float* __restrict__ b_hh, int bx, int by, int B, int H) {
+        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+        const int g = lane >> 4, c = lane & 15;
+        const int n0 = bx * (16 * NT), r0 = by * (16 * RB);
+        const int kbeg = w * (H / RSM_WAVES);
+        // this wave's W_hh slice: chunk i, tile nt, MFMA j -> W[kbeg + 16 i + 4 g + j][n0 + 16 nt + c]
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-        const int e = tid + k * 64 * RSM_WAVES;
-        const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
-        const int rb = tl / NT, nt = tl - rb * NT;
-        const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
-        eoff[k] = (r * H + n) * 4;   // rows past B: past the resource (load 0, store dropped)
-        etl[k] = tl;
-        el[k] = l;
-        ej[k] = j;
-        ebias[k] = b_hh[n] + b_ih[n];
+        for (int i = 0; i < KCH; i++)
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) bw[i][nt][j] = Whh[(long)(kbeg + 16 * i + 4 * g + j) * H + n0 + 16 * nt + c];
+        // row offsets (floats) of this lane's A rows: rows past B read row B - 1 (never stored)
+#pragma unroll
+        for (int rb = 0; rb < RB; rb++) arow[rb] = min(r0 + rb * 16 + c, B - 1) * H + kbeg + 4 * g;
+        // this thread's outputs: their byte offset in a frame and (b_hh + b_ih)
+#pragma unroll
+        for (int k = 0; k < EPT; k++) {
+            const int e = tid + k * 64 * RSM_WAVES;
+            const int tl = e >> 8, j = (e >> 6) & 3, l = e & 63;
+            const int rb = tl / NT, nt = tl - rb * NT;
+            const int r = r0 + rb * 16 + (l >> 4) * 4 + j, n = n0 + nt * 16 + (l & 15);
+            eoff[k] = (r * H + n) * 4;   // rows past B: past the resource (load 0, store dropped)
+            etl[k] = tl;
+            el[k] = l;
+            ej[k] = j;
+            ebias[k] = b_hh[n] + b_ih[n];
+        }
     }
-    for (int t = 0; t < T; t++) {
-        float* ht = hid + (long)t * slab;
-        const float* hp = t > 0 ? hid + (long)(t - 1) * slab : h0;
-        // P_t (the input projection, in place in h_t) does not depend on
-        // h_{t-1}: loaded before the wait for frame t - 1
-        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(ht, (short)0, sbytes, 0x00020000);
-        float Pv[EPT];
+
+    // P_t of this thread's outputs (coherent loads)
+    __device__ __forceinline__ void load_p(__amdgpu_buffer_rsrc_t rs_t, float (&Pv)[EPT]) const {
 #pragma unroll
         for (int k = 0; k < EPT; k++)
             Pv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_t, eoff[k], 0, RP_SC1));
-        if (t > 0) {   // every workgroup has published frame t - 1
-            if (tid == 0) {
-                const unsigned target = nwg * (unsigned)t;
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {   // 0.5 s at 100 MHz
-                        rp_abort = 1;
-                        __hip_atomic_store(timeout_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        break;
-                    }
-                }
-            }
-            __syncthreads();
-            if (rp_abort) return;
-        }
+    }
+
+    // h_t = tanhf((P_t + h_{t-1}.W_hh) + bias) of this thread's outputs (hp:
+    // h_{t-1}; NULL: h_{-1} = 0, bias_tanh's formula), stored write-through.
+    // rp_part: the workgroup's partial products (LDS); one barrier inside.
+    __device__ __forceinline__ void frame(const float* hp, int sbytes, __amdgpu_buffer_rsrc_t rs_t,
+                                          const float (&Pv)[EPT], f32x4* rp_part) const {
+        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
         if (hp) {
             const auto rs_p = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hp), (short)0, sbytes, 0x00020000);
             f32x4 acc[RB][NT];
@@ -1282,65 +1288,178 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rs_t, eoff[k], 0, RP_SC1);
             }
         }
-        // publish frame t: every wave's stores drained, then one add per workgroup
+    }
+};
+
+// fault_frame >= 1 (test hook ASR_RNN_PERSIST_FAULT): workgroup (0, 0)
+// stalls before that frame, as if it had lost its CU, until the others give
+// up (bounded: 2 s); then the launch ends aborted and the recovery kernel
+// finishes it.
+template <int RB, int NT, int KCH>
+__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const float* h0,
+                                                                          const float* __restrict__ Whh,
+                                                                          const float* __restrict__ b_ih,
+                                                                          const float* __restrict__ b_hh,
+                                                                          float* hid, int T, int B, int H,
+                                                                          PersistCtl* ctl, int* host_status,
+                                                                          int fault_frame) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 rp_part[];   // [RSM_WAVES][RB * NT][64], then the abort flag
+    int& rp_abort = *reinterpret_cast<int*>(rp_part + RSM_WAVES * RB * NT * 64);
+    using Tile = RpTile<RB, NT, KCH>;
+    constexpr int EPT = Tile::EPT;
+    const int tid = threadIdx.x;
+    const unsigned nwg = gridDim.x * gridDim.y;
+    const unsigned wg = blockIdx.y * gridDim.x + blockIdx.x;
+    Tile tile;
+    tile.setup(Whh, b_ih, b_hh, blockIdx.x, blockIdx.y, B, H);
+    if (tid == 0)   // dispatched after the launch gave up: leave every frame to the recovery
+        rp_abort = (int)__hip_atomic_load(&ctl->abort, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (rp_abort) return;
+    const long slab = (long)B * H;
+    const int sbytes = (int)(slab * 4);
+    for (int t = 0; t < T; t++) {
+        float* ht = hid + (long)t * slab;
+        const float* hp = t > 0 ? hid + (long)(t - 1) * slab : h0;
+        // P_t (the input projection, in place in h_t) does not depend on
+        // h_{t-1}: loaded before the wait for frame t - 1
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(ht, (short)0, sbytes, 0x00020000);
+        float Pv[EPT];
+        tile.load_p(rs_t, Pv);
+        if (t > 0) {   // every workgroup has published frame t - 1
+            if (tid == 0) {
+                const unsigned target = nwg * (unsigned)t;
+                unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                if (t == fault_frame && wg == 0) {   // test hook: stall until the launch is aborted
+                    while (!__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                           __builtin_amdgcn_s_memrealtime() - t0 < 4 * RP_TIMEOUT)
+                        __builtin_amdgcn_s_sleep(8);
+                    rp_abort = 1;
+                }
+                while (!rp_abort && __hip_atomic_load(&ctl->ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        rp_abort = 1;
+                    } else if (__builtin_amdgcn_s_memrealtime() - t0 > RP_TIMEOUT) {
+                        rp_abort = 1;
+                        __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(host_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+            }
+            __syncthreads();
+            if (rp_abort) return;
+        }
+        tile.frame(hp, sbytes, rs_t, Pv, rp_part);
+        // publish frame t: every wave's stores drained, then the workgroup's
+        // progress and one add to the counter
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            __hip_atomic_store(&ctl->prog[wg], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
-// The timeout flag in pinned, device-mapped host memory: the host reads it
-// with no HIP call (a synchronous copy would wait for every stream's work).
-static int* persist_flag_host = nullptr;
-static int* persist_flag_dev = nullptr;
-static int persist_flag(int** dev) {
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!persist_flag_host) {
-        void* h = nullptr;
-        ASR_HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(h, 0, 64);
-        void* d = nullptr;
-        ASR_HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
-        persist_flag_host = static_cast<int*>(h);
-        persist_flag_dev = static_cast<int*>(d);
+// After every one-launch recurrence, on its stream: nothing unless the launch
+// was aborted; then ONE workgroup computes, frame by frame, every tile's
+// frames from its prog[] on, with the persistent kernel's per-tile code (the
+// W_hh slice reloaded per tile), so the bits are those of a complete launch.
+template <int RB, int NT, int KCH>
+__global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_recover_kernel(const float* h0,
+                                                                          const float* __restrict__ Whh,
+                                                                          const float* __restrict__ b_ih,
+                                                                          const float* __restrict__ b_hh,
+                                                                          float* hid, int T, int B, int H,
+                                                                          int gx, int gy, PersistCtl* ctl) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 rp_part[];
+    if (!__hip_atomic_load(&ctl->abort, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) return;
+    using Tile = RpTile<RB, NT, KCH>;
+    constexpr int EPT = Tile::EPT;
+    const int nwg = gx * gy;
+    const long slab = (long)B * H;
+    const int sbytes = (int)(slab * 4);
+    unsigned tmin = (unsigned)T;
+    for (int q = 0; q < nwg; q++) tmin = min(tmin, __hip_atomic_load(&ctl->prog[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int t = (int)tmin; t < T; t++) {
+        float* ht = hid + (long)t * slab;
+        const float* hp = t > 0 ? hid + (long)(t - 1) * slab : h0;
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(ht, (short)0, sbytes, 0x00020000);
+        for (int q = 0; q < nwg; q++) {
+            if (__hip_atomic_load(&ctl->prog[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (unsigned)t) continue;
+            Tile tile;
+            tile.setup(Whh, b_ih, b_hh, q % gx, q / gx, B, H);
+            float Pv[EPT];
+            tile.load_p(rs_t, Pv);
+            tile.frame(hp, sbytes, rs_t, Pv, rp_part);
+            __syncthreads();   // rp_part is the next tile's
+        }
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // frame t stored before any load of it
     }
-    *dev = persist_flag_dev;
-    return ASR_OK;
 }
+
+// Per-launch control blocks: a launch owns one from its memset until an event
+// recorded after its recovery kernel completes; only then is it handed out
+// again (several pipelines, streams or threads may have launches in flight).
+// The status word sits in pinned, device-mapped host memory, so reading it
+// takes no HIP call.
+namespace {
+struct PersistSlot {
+    PersistCtl* ctl = nullptr;
+    int* status_h = nullptr;   // host view
+    int* status_d = nullptr;   // device view
+    hipEvent_t done = nullptr;
+    bool used = false;
+    int nwg = 0;               // workgroups of its launch
+    bool plain = false;        // a launch without a pipeline CU hint
+};
+struct PersistPool {
+    std::mutex mu;
+    std::vector<PersistSlot> slots[64];
+    long long launches = 0, recoveries = 0;
+};
+PersistPool& persist_pool() {
+    static PersistPool* p = new PersistPool();   // never destroyed: slots outlive static destructors
+    return *p;
+}
+// a completed slot: count its recovery, clear it (mu held)
+bool persist_reap(PersistPool& pp, PersistSlot& s) {
+    if (!s.used) return true;
+    if (hipEventQuery(s.done) != hipSuccess) return false;
+    if (__atomic_load_n(s.status_h, __ATOMIC_ACQUIRE)) {
+        pp.recoveries++;
+        __atomic_store_n(s.status_h, 0, __ATOMIC_RELEASE);
+    }
+    s.used = false;
+    return true;
+}
+}  // namespace
 
 template <int RB, int NT, int KCH>
 static int launch_persist(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
-                          int T, int B, int H, unsigned* ctr, hipStream_t s) {
-    static AsrAttrOnce attr;
+                          int T, int B, int H, PersistSlot& slot, int fault_frame, hipStream_t s) {
+    static AsrAttrOnce attr, attr_r;
     if (int r_ = attr.set((const void*)rnn_recur_persist_kernel<RB, NT, KCH>, RP_LDS)) return r_;
-    int* flag = nullptr;
-    if (int r_ = persist_flag(&flag)) return r_;
-    hipLaunchKernelGGL((rnn_recur_persist_kernel<RB, NT, KCH>), dim3((unsigned)(H / (16 * NT)), (unsigned)((B + 16 * RB - 1) / (16 * RB))),
-                       dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, flag);
+    if (int r_ = attr_r.set((const void*)rnn_recur_recover_kernel<RB, NT, KCH>, RP_LDS)) return r_;
+    static std::once_flag occ_once;
+    static int occ = 0;
+    std::call_once(occ_once, [] {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, rnn_recur_persist_kernel<RB, NT, KCH>,
+                                                         64 * RSM_WAVES, RP_LDS) != hipSuccess)
+            occ = 0;
+    });
+    if (occ < 1) return ASR_ERR_UNSUPPORTED;   // one workgroup must fit a CU
+    const int gx = H / (16 * NT), gy = (B + 16 * RB - 1) / (16 * RB);
+    ASR_HIP_TRY(hipMemsetAsync(slot.ctl, 0, offsetof(PersistCtl, prog) + sizeof(unsigned) * gx * gy, s));
+    hipLaunchKernelGGL((rnn_recur_persist_kernel<RB, NT, KCH>), dim3((unsigned)gx, (unsigned)gy),
+                       dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh, b_ih, b_hh, hid, T, B, H, slot.ctl, slot.status_d,
+                       fault_frame);
     ASR_LAUNCH_TRY();
-    return ASR_OK;
-}
-
-// Step counters, one per launch in flight (a ring; zeroed on the stream
-// before each launch).
-static int persist_counter(hipStream_t s, unsigned** out) {
-    static std::mutex mu;
-    static unsigned* ring[16] = {};
-    static unsigned next[16] = {};
-    int dev = 0;
-    ASR_HIP_TRY(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 16) return ASR_ERR_UNSUPPORTED;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!ring[dev]) {
-        void* p = nullptr;
-        ASR_HIP_TRY(hipMalloc(&p, 64 * 256));
-        ASR_HIP_TRY(hipMemset(p, 0, 64 * 256));
-        ring[dev] = static_cast<unsigned*>(p);
-    }
-    unsigned* c = ring[dev] + 16 * (next[dev]++ % 64);   // 64-byte slots
-    ASR_HIP_TRY(hipMemsetAsync(c, 0, 16, s));
-    *out = c;
+    hipLaunchKernelGGL((rnn_recur_recover_kernel<RB, NT, KCH>), dim3(1), dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh,
+                       b_ih, b_hh, hid, T, B, H, gx, gy, slot.ctl);
+    ASR_LAUNCH_TRY();
     return ASR_OK;
 }
 
@@ -1353,11 +1472,29 @@ int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_i
     if (T < 2 || B <= 0 || B > 256 || (H % 128) != 0 || H < 384 || H > 1024 || ((uintptr_t)hid % 16) != 0 ||
         (h0 && ((uintptr_t)h0 % 16) != 0) || (long)B * H * 4 >= 0x7fffffffL)
         return ASR_ERR_UNSUPPORTED;
+    // a captured graph would replay one control block for ever: per-frame steps there
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return ASR_ERR_UNSUPPORTED;
     const int nwg = (H / 32) * ((B + 15) / 16);
-    if (cus <= 0) {   // no hint: half of the CUs the stream's mask allows (room beside it)
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return ASR_ERR_UNSUPPORTED;
+    int dev = 0;
+    ASR_HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return ASR_ERR_UNSUPPORTED;
+    const bool plain = cus <= 0;
+    PersistPool& pp = persist_pool();
+    std::lock_guard<std::mutex> lock(pp.mu);
+    auto& slots = pp.slots[dev];
+    PersistSlot* slot = nullptr;
+    int reserved = 0;   // workgroups of plain launches still in flight on this device
+    for (auto& q : slots) {
+        if (persist_reap(pp, q)) {
+            if (!slot) slot = &q;
+        } else if (q.plain) {
+            reserved += q.nwg;
+        }
+    }
+    if (plain) {   // no hint: half of the CUs the stream's mask allows (room beside it), less other plain launches'
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return ASR_ERR_UNSUPPORTED;
         int avail = ncu;
         if (s) {   // a caller's CU-masked stream
             uint32_t m[32] = {};
@@ -1368,23 +1505,51 @@ int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_i
                 if (n > 0) avail = std::min(avail, n);
             }
         }
-        cus = avail / 2;
+        cus = avail / 2 - reserved;
     }
     if (nwg > cus) return ASR_ERR_UNSUPPORTED;   // every workgroup resident at once
-    unsigned* ctr = nullptr;
-    if (int rc = persist_counter(s, &ctr)) return rc;
-    switch (H / 128) {
-        case 3: return launch_persist<1, 2, 3>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
-        case 4: return launch_persist<1, 2, 4>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
-        case 5: return launch_persist<1, 2, 5>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
-        case 6: return launch_persist<1, 2, 6>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
-        case 7: return launch_persist<1, 2, 7>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
-        default: return launch_persist<1, 2, 8>(h0, Whh, b_ih, b_hh, hid, T, B, H, ctr, s);
+    if (!slot) {
+        PersistSlot n;
+        ASR_HIP_TRY(hipMalloc(&n.ctl, sizeof(PersistCtl)));
+        void* h = nullptr;
+        ASR_HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(h, 0, 64);
+        n.status_h = static_cast<int*>(h);
+        void* d = nullptr;
+        ASR_HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
+        n.status_d = static_cast<int*>(d);
+        ASR_HIP_TRY(hipEventCreateWithFlags(&n.done, hipEventDisableTiming));
+        slots.push_back(n);
+        slot = &slots.back();
     }
+    // test hook: ASR_RNN_PERSIST_FAULT=<frame> stalls one workgroup before that frame
+    const char* fe = getenv("ASR_RNN_PERSIST_FAULT");
+    const int fault_frame = fe ? atoi(fe) : -1;
+    int rc;
+    switch (H / 128) {
+        case 3: rc = launch_persist<1, 2, 3>(h0, Whh, b_ih, b_hh, hid, T, B, H, *slot, fault_frame, s); break;
+        case 4: rc = launch_persist<1, 2, 4>(h0, Whh, b_ih, b_hh, hid, T, B, H, *slot, fault_frame, s); break;
+        case 5: rc = launch_persist<1, 2, 5>(h0, Whh, b_ih, b_hh, hid, T, B, H, *slot, fault_frame, s); break;
+        case 6: rc = launch_persist<1, 2, 6>(h0, Whh, b_ih, b_hh, hid, T, B, H, *slot, fault_frame, s); break;
+        case 7: rc = launch_persist<1, 2, 7>(h0, Whh, b_ih, b_hh, hid, T, B, H, *slot, fault_frame, s); break;
+        default: rc = launch_persist<1, 2, 8>(h0, Whh, b_ih, b_hh, hid, T, B, H, *slot, fault_frame, s); break;
+    }
+    if (rc) return rc;
+    ASR_HIP_TRY(hipEventRecord(slot->done, s));
+    slot->used = true;
+    slot->nwg = nwg;
+    slot->plain = plain;
+    pp.launches++;
+    return ASR_OK;
 }
 
-int rnn_persist_status(int* timed_out) {
-    *timed_out = persist_flag_host ? __atomic_load_n(persist_flag_host, __ATOMIC_ACQUIRE) : 0;
+int rnn_persist_stats(long long* launches, long long* recoveries) {
+    PersistPool& pp = persist_pool();
+    std::lock_guard<std::mutex> lock(pp.mu);
+    for (auto& v : pp.slots)
+        for (auto& q : v) persist_reap(pp, q);
+    if (launches) *launches = pp.launches;
+    if (recoveries) *recoveries = pp.recoveries;
     return ASR_OK;
 }
 

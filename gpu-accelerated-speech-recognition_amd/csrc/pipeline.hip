@@ -484,14 +484,9 @@ int fetch_to(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, do
     asr_ctc_t* h = p->dec[j % p->nbuf];
     *res_rc = asr_ctc_get_best(h, labels, max_len, lengths, logp);
     if (*res_rc != ASR_OK && *res_rc != ASR_ERR_BEAM_OVERFLOW) return *res_rc;
-    if (p->cfg.H > 256) {   // a one-launch recurrence that gave up waiting for its workgroups (never expected)
-        int timed_out = 0;
-        if (int r = asr::rnn_persist_status(&timed_out)) return r;
-        if (timed_out) {
-            set_failed(p, j, ASR_ERR_INTERNAL);
-            return ASR_ERR_INTERNAL;
-        }
-    }
+    // (a one-launch H > 256 recurrence that gave up waiting for its
+    // workgroups was finished by its recovery kernel before the emission
+    // projection read it: asr_rnn_persist_stats counts those)
     if (ms) asr_ctc_last_kernel_ms(h, ms);
     if (p->timing && j >= p->timing_from) {   // the batch's stamps, all complete once its decode is
         const int k = (int)(j % p->nbuf);

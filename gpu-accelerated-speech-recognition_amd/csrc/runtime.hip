@@ -392,6 +392,10 @@ int asr_rnn_recur_fwd(const float* h0, const float* W_hh, const float* b_ih, con
     return rnn_recurrence(h0, W_hh, b_ih, b_hh, hid, T, B, H, asr_stream(s));
 }
 
+int asr_rnn_persist_stats(long long* launches, long long* recoveries) {
+    return asr::rnn_persist_stats(launches, recoveries);
+}
+
 int asr_rnn_emit_fwd(const float* h0, const float* W_hh, const float* b_ih, const float* b_hh,
                      const float* W_out, const float* b_out, const float* P, float* hiddens,
                      float* emis, int T, int B, int H, int V, asr_stream_t s) {

@@ -122,6 +122,22 @@ int asr_rnn_fwd(const float* d_x, const float* d_h0, const float* d_W_ih, const 
 int asr_rnn_recur_fwd(const float* d_h0, const float* d_W_hh, const float* d_b_ih,
                       const float* d_b_hh, float* d_hiddens, int T, int B, int H, asr_stream_t s);
 
+/* For 384 <= H <= 1024 (H % 128 == 0, B <= 256) asr_rnn_fwd / asr_rnn_recur_fwd
+ * run the whole recurrence in ONE launch whose workgroups hand h_t to each
+ * other (W_hh resident in registers); it is taken only when its H/32 x
+ * ceil(B/16) workgroups fit the CUs the stream may use (half of them for a
+ * plain call, less other such launches in flight; the pipeline's share for
+ * its own), never while the stream is capturing.  Residency is still not
+ * guaranteed (other processes, other work on those CUs), so a launch that
+ * waits 0.5 s without progress gives up and a one-workgroup recovery kernel
+ * queued behind it on the same stream finishes the frames it had not
+ * published, with the same arithmetic: the call's result is always the
+ * complete recurrence, bit for bit (never a partial h with ASR_OK), only
+ * slower.  This reports how many such launches ran and how many completed
+ * through the recovery (counted once their stream has passed them).
+ * (Replaces nothing in the reference: RNN.cu:9-30 launched T steps.) */
+int asr_rnn_persist_stats(long long* launches, long long* recoveries);
+
 /* Recurrence kernel choice for H <= 256 (H % 16 == 0), process-wide:
  * ASR_RNN_RECUR_VALU — one utterance per CU, W_hh in registers: the shortest
  *   step (~0.7-0.9 us), a whole CU per utterance;

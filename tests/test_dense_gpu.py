@@ -450,6 +450,49 @@ def test_rnn_persistent_recurrence_same_bits(T, B, H, with_h0, monkeypatch):
         close(outs[0], _torch_rnn(x, T, B, w_ih, w_hh, b_ih, b_hh, h0), 1e-4)
 
 
+def test_rnn_persistent_recurrence_fault_recovers(monkeypatch):
+    """The one-launch recurrence is fail-safe:
+    the test hook ASR_RNN_PERSIST_FAULT=<frame> makes one workgroup stall
+    before that frame as if it had lost its CU; the others give up after 0.5 s
+    without progress, the launch ends aborted and the recovery kernel queued
+    behind it finishes the frames no tile had published.  The plain call
+    (asr_rnn_fwd, RNN::forward's path) returns the complete recurrence, bit for
+    bit the per-frame steps', within about a second; asr_rnn_persist_stats
+    counts the recovery; the next call in the process is an ordinary
+    one-launch recurrence with the same bits and no recovery."""
+    import time
+    monkeypatch.setenv("ASR_RNN_GRAPH", "0")
+    T, B, I, H = 200, 32, 64, 1024
+    rng = np.random.default_rng(2026)
+    x = rng.uniform(-1, 1, (T * B, I)).astype(np.float32)
+    s = 1 / np.sqrt(H)
+    W = [dm(rng.uniform(-s, s, (I, H)).astype(np.float32)), dm(rng.uniform(-s, s, (H, H)).astype(np.float32)),
+         dm(rng.uniform(-0.1, 0.1, (H, 1)).astype(np.float32)), dm(rng.uniform(-0.1, 0.1, (H, 1)).astype(np.float32))]
+    dx = dm(x)
+    monkeypatch.setenv("ASR_RNN_PERSIST", "0")
+    ref = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dx, *W, ref, T, B)
+    ref = ref.toCpu()
+    monkeypatch.setenv("ASR_RNN_PERSIST", "1")
+    n0, r0 = asr.rnn_persist_stats()
+    monkeypatch.setenv("ASR_RNN_PERSIST_FAULT", "117")
+    got = asr.DeviceMatrix(T * B, H)
+    t0 = time.perf_counter()
+    asr.rnn_fwd(dx, *W, got, T, B)
+    out = got.toCpu()
+    dt = time.perf_counter() - t0
+    monkeypatch.delenv("ASR_RNN_PERSIST_FAULT")
+    n1, r1 = asr.rnn_persist_stats()
+    assert (n1 - n0, r1 - r0) == (1, 1), (n0, r0, n1, r1)
+    assert np.array_equal(out, ref)
+    assert 0.4 < dt < 3.0, dt   # the 0.5 s give-up, then the recovery
+    again = asr.DeviceMatrix(T * B, H)
+    asr.rnn_fwd(dx, *W, again, T, B)
+    assert np.array_equal(again.toCpu(), ref)
+    n2, r2 = asr.rnn_persist_stats()
+    assert (n2 - n1, r2 - r1) == (1, 0)
+
+
 def test_rnn_persistent_recurrence_on_a_masked_stream(monkeypatch):
     """A caller's CU-masked stream with fewer CUs than the one-launch
     recurrence has workgroups (C5's 64 on a 32-CU stream): the launcher reads

@@ -213,6 +213,38 @@ def test_pipeline_segmented_handoff(segments, B):
         assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
 
 
+def test_pipeline_persistent_recurrence_fault_recovers(monkeypatch):
+    """The pipeline path of the fail-safe one-launch recurrence (H > 256,
+    C5-like): batch 1's recurrence launches run with one workgroup stalled
+    (ASR_RNN_PERSIST_FAULT), give up and are finished by their recovery
+    kernels; every batch — the faulted one and the later ones — collects the
+    sequential path's bits, and nothing fails the pipeline."""
+    T, B, inp, H, V, beam = 24, 16, 32, 384, 100, 12
+    W = _weights(inp, H, V, seed=41)
+    rng = np.random.default_rng(41)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(4)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W)
+    d = p.describe()
+    assert d["mode"] == "CU groups (H > 256)", d
+    n0, r0 = asr.rnn_persist_stats()
+    got = []
+    for i, x in enumerate(xs):
+        if i == 1:
+            monkeypatch.setenv("ASR_RNN_PERSIST_FAULT", "5")
+        p.submit(x)
+        monkeypatch.delenv("ASR_RNN_PERSIST_FAULT", raising=False)
+    while p.pending():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+    p.close()
+    n1, r1 = asr.rnn_persist_stats()
+    assert n1 - n0 == 4 * d["segments"], (n0, n1, d)   # one launch per batch and T-segment
+    assert r1 - r0 >= 1, (r0, r1)                      # batch 1's segments that reached frame 5
+    for g, x in zip(got, xs):
+        ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_AUTO)
+        assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
+
+
 @pytest.mark.parametrize("group", ["2", "3"])
 def test_pipeline_production_groups(group, monkeypatch):
     """H > 256 (C5-like): the recurrences of G consecutive batches run as one
