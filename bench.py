@@ -405,27 +405,33 @@ class ClockSampler:
                 "hotspot_c_max": round(float(max(tp)), 1) if tp else None}
 
 
-def serialized_decode(asr, em_host, T, Bp, V, beam, dcus, conc, reps=2):
-    """The decoder alone, live, after the timed region: `conc` decodes of the
-    last batch's emissions at once, one per stream over the pipeline's decode
-    CUs [0, dcus) (the decodes the pipeline keeps resident there: 16
-    utterances per CU), with the pipeline's decoder schedule; HIP events on
-    those streams.  Returns ms per decode launch (the max over the streams of
-    a round, divided by conc) — the kernel's own time at the pipeline's load,
-    without the queue wait the timed region's event spans include."""
+def serialized_decode(asr, em_host, T, Bp, V, beam, dcus, conc, queued=2, rounds=3):
+    """The decoder alone, live, after the timed region, at the pipeline's load:
+    the last batch's emissions decoded on conc + queued streams over the
+    pipeline's decode CUs [0, dcus) (conc decodes are what those CUs hold at
+    16 utterances per CU; the pipeline keeps `queued` more waiting so that
+    their workgroups fill the CUs the oldest decodes' last utterances free),
+    `rounds` decodes back to back on every stream, with the pipeline's decoder
+    schedule; HIP events on those streams.  Returns ms per decode launch: the
+    wall time of all rounds / (rounds x streams), i.e. the kernel's throughput
+    with its dispatch tails filled as in the pipeline and nothing else
+    running."""
     d_em = asr.DeviceMatrix.from_numpy(np.ascontiguousarray(em_host).reshape(T * Bp, V))
-    sts = [cu_range_stream(0, dcus) for _ in range(conc)]
-    decs = [asr.CTCDecoder(V, beam, 0, waves=asr.ASR_CTC_WAVES_LIST) for _ in range(conc)]
+    ns = conc + queued
+    sts = [cu_range_stream(0, dcus) for _ in range(ns)]
+    # one handle per stream: its decodes run one after another there
+    decs = [asr.CTCDecoder(V, beam, 0, waves=asr.ASR_CTC_WAVES_LIST) for _ in range(ns)]
     for d in decs:
         d.set_concurrency(conc)
     best = None
-    for _ in range(reps + 1):   # the first round sizes the workspaces
+    for _ in range(2):   # the first pass sizes the workspaces
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record(sts[0])
         ends = []
         for st, d in zip(sts, decs):
             st.wait_event(e0)
-            d.decode_device(d_em.ptr, T, Bp, is_log=True, stream=st.cuda_stream)
+            for _ in range(rounds):
+                d.decode_device(d_em.ptr, T, Bp, is_log=True, stream=st.cuda_stream)
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(st)
             ends.append(e1)
@@ -435,7 +441,7 @@ def serialized_decode(asr, em_host, T, Bp, V, beam, dcus, conc, reps=2):
         best = ms if best is None else min(best, ms)
     for d in decs:
         d.close()
-    return best / conc
+    return best / (rounds * ns)
 
 
 def union_ms(iv):
@@ -451,7 +457,7 @@ def union_ms(iv):
     return tot
 
 
-def stage_figures(stamps, elapsed_ms, host_wait_ms, steps, nsub):
+def stage_figures(stamps, elapsed_ms, host_wait_ms, steps, nsub, inflight):
     """Per-stage figures of the timed region from the pipeline's timeline
     (asr_pipeline_get_timeline: per batch, ms after the region's start, of
     its production start / end and decode start / end) and the host's time
@@ -460,9 +466,20 @@ def stage_figures(stamps, elapsed_ms, host_wait_ms, steps, nsub):
         return None
     t = np.asarray(stamps, np.float64)
     prod, dec = t[:, 1] - t[:, 0], t[:, 3] - t[:, 2]
+    # steady state: the mean spacing of decode ends (in time order) over the
+    # middle half of the batches, i.e. without the fill and the drain; with
+    # fewer than 3 x inflight batches there is no such middle (every batch is
+    # in the fill or the drain: the 256-per-GPU shard's 20 batches at 10 in
+    # flight), and the figure is null
+    n = len(t)
+    steady = None
+    if n >= 3 * max(1, inflight) and n >= 4:
+        ends = np.sort(t[:, 3])
+        lo, hi = n // 4, (3 * n) // 4
+        steady = round(float((ends[hi] - ends[lo]) / (hi - lo) * nsub), 4)
     return {
         "source": "HIP timing events recorded by the pipeline in the timed run (asr_pipeline_set_timing)",
-        "batches": int(len(t)),
+        "batches": int(n),
         "production_ms_per_batch": round(float(prod.mean()), 4),
         "decode_span_ms_per_batch": round(float(dec.mean()), 4),
         "production_busy_frac": round(union_ms(list(zip(t[:, 0], t[:, 1]))) / elapsed_ms, 4),
@@ -470,10 +487,11 @@ def stage_figures(stamps, elapsed_ms, host_wait_ms, steps, nsub):
         "first_decode_start_ms": round(float(t[:, 2].min()), 4),
         "last_production_end_ms": round(float(t[:, 1].max()), 4),
         "last_decode_end_ms": round(float(t[:, 3].max()), 4),
-        "steady_ms_per_step": (round(float((t[-1, 3] - t[nsub - 1, 3]) / (steps - 1)), 4) if steps > 1 else None),
+        "steady_ms_per_step": steady,
         "host_wait_ms_per_step": round(host_wait_ms / steps, 4),
         "note": "a decode's start is when its stream reached it (it may then wait for CUs); steady_ms_per_step "
-                "= decode ends of the first to the last step over steps - 1 (no fill, no drain)"}
+                "= mean spacing of the decode ends over the middle half of the batches x batches per step "
+                "(null below 3 x inflight batches)"}
 
 
 def cpu_model() -> str:
@@ -996,7 +1014,7 @@ def finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elap
     d_x, d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout = weights
     # per-stage spans, clock and CU placement of the timed run: top-level fields of the line
     sched = dict(sched or {})
-    measured = {k: sched.pop(k) for k in ("stages", "clock", "cu_placement") if k in sched}
+    measured = {k: sched.pop(k) for k in ("stages", "clock", "cu_placement", "host") if k in sched}
     ser = sched.pop("serialized", None)
     DM = asr.DeviceMatrix.from_numpy
     # ---- host-side gather of the hypotheses (outside the timed region)
@@ -1236,16 +1254,18 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
         pl.set_timing(True)
     clock.start()
     take.wait = 0.0
+    c0 = time.process_time()
     t0 = time.perf_counter()
     run(args.steps)
     asr.synchronize()
     elapsed = time.perf_counter() - t0
+    host_cpu_ms = 1e3 * (time.process_time() - c0) / args.steps
     clock_fig = clock.stop()
     gc.enable()
     stages = None
     if timeline:
         _, stamps = pl.timeline()
-        stages = stage_figures(stamps, 1e3 * elapsed, 1e3 * take.wait, args.steps, nsub)
+        stages = stage_figures(stamps, 1e3 * elapsed, 1e3 * take.wait, args.steps, nsub, desc["inflight"])
         if os.environ.get("ASR_BENCH_TIMELINE"):   # diagnostics: the raw per-batch stamps
             np.savetxt(os.environ["ASR_BENCH_TIMELINE"], stamps, fmt="%.4f",
                        header="production start, production end, decode start, decode end (ms)")
@@ -1262,6 +1282,10 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             for what, tt in hostlog:
                 f.write(f"{what} {1e3 * (tt - t0):.3f}\n")
     elapsed = reduce_max_over_ranks(elapsed, world)
+    host = {"cpu_ms_per_step": round(host_cpu_ms, 4),
+            "cpu_ms_per_step_max_over_ranks": round(reduce_max_over_ranks(host_cpu_ms, world), 4),
+            "how": "time.process_time() of the rank's process (all its threads) over the timed region / steps: "
+                   "the host CPU one rank spends per step (an 8-rank node shares its host cores)"}
     if world > 1:
         dist.barrier()
     desc = pl.describe()
@@ -1296,11 +1320,14 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             and not args.no_serialized):
         dc = desc["decode_cus"]
         conc = max(1, (16 if kcap <= 64 else 9) * dc // Bp)   # the decodes the decode CUs hold
+        queued = max(0, desc["inflight"] - conc)
         ms1 = serialized_decode(asr, em_last[0] if em_last is not None else pl.peek_emissions(), T, Bp, V, beam,
-                                dc, conc)
-        ser = {"ms_per_launch": round(ms1, 4), "concurrent": conc, "decode_cus": dc,
-               "how": f"{conc} decodes of the last batch's emissions at once on the {dc} decode CUs, "
-                      f"nothing else running (HIP events, live after the timed region)"}
+                                dc, conc, queued=queued)
+        ser = {"ms_per_launch": round(ms1, 4), "concurrent": conc, "queued": queued, "decode_cus": dc,
+               "how": f"{conc + queued} streams over the {dc} decode CUs ({conc} decodes resident at 16 per "
+                      f"CU, {queued} queued, as in the pipeline), 3 decodes of the last batch's emissions back "
+                      f"to back on each, nothing else running: wall / decodes (HIP events, live after the timed "
+                      f"region)"}
     finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
            (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_last,
            {"pipeline_batch": Bp, "batches_per_step": nsub,
@@ -1309,7 +1336,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
             "segments": desc.get("segments"),
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
-            "stages": stages, "clock": clock_fig, "cu_placement": placement, "serialized": ser,
+            "stages": stages, "clock": clock_fig, "cu_placement": placement, "serialized": ser, "host": host,
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "
                         f"{desc['decode_cus']} CUs, {desc['prod_streams']} production stream(s); "
                         f"library-owned streams, buffers and decoder schedule"},
@@ -1472,9 +1499,11 @@ def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V
     st = torch.cuda.current_stream()
     split = asr.get_dense_arith() == asr.DENSE_SPLIT_BF16
     out = {"arith": "split_bf16" if split else "f32",
-           "note": "tflops = fp32 FLOP / s against the fp32 MFMA peak (mfma_util); on the split "
-                   "arithmetic each fp32 product is 6 bf16 MFMA products (bf16_mfma_util against "
-                   "the dense bf16 peak)" if split else "tflops = fp32 FLOP / s against the fp32 MFMA peak"}
+           "note": "tflops = the stage's fp32 FLOP / s.  On the split arithmetic each fp32 product is 6 bf16 "
+                   "MFMA products: mfma_util = 6 x tflops over the dense bf16 peak (the matrix cores' real "
+                   "use); fp32_equiv_vs_fp32_peak = tflops over the fp32 MFMA peak (can exceed 1: fp32 "
+                   "results from bf16 matrix cores, not fp32 MFMA utilisation)" if split
+                   else "tflops = fp32 FLOP / s; mfma_util against the fp32 MFMA peak"}
     stages = [
         ("input_gemm", lambda: asr.linear_fwd(d_x, d_wih, None, d_hid, asr.EPI_NONE, st.cuda_stream),
          2.0 * T * B * In * H),
@@ -1500,12 +1529,15 @@ def measure_gemms(asr, d_x, d_wih, d_hid, d_wout, d_bout, d_emis, T, B, In, H, V
                      "mfma_util": round(tf / FP32_MFMA_PEAK_TF, 4),
                      "hbm_gbs": round(hbm / (us * 1e-6) / 1e9, 1)}
         if split and name != "emission_gemm":   # fp32 work on the bf16 matrix cores, 6 products each
+            out[name]["fp32_equiv_vs_fp32_peak"] = out[name]["mfma_util"]
             out[name]["bf16_mfma_tflops"] = round(SPLIT_PRODUCTS * tf, 1)
-            out[name]["bf16_mfma_util"] = round(SPLIT_PRODUCTS * tf / BF16_MFMA_PEAK_TF, 4)
+            out[name]["mfma_util"] = round(SPLIT_PRODUCTS * tf / BF16_MFMA_PEAK_TF, 4)
+            out[name]["peak"] = "dense bf16 MFMA"
         if name == "recurrence_emission":   # per busy CU: one 16-utterance workgroup per CU
             busy = min(-(-B // 16), torch.cuda.get_device_properties(st.device).multi_processor_count)
             ncu = torch.cuda.get_device_properties(st.device).multi_processor_count
-            out[name]["mfma_util_busy_cus"] = round(tf / (FP32_MFMA_PEAK_TF * busy / ncu), 4)
+            peak = BF16_MFMA_PEAK_TF / SPLIT_PRODUCTS if split else FP32_MFMA_PEAK_TF
+            out[name]["mfma_util_busy_cus"] = round(tf / (peak * busy / ncu), 4)
             out[name]["busy_cus"] = busy
     return out
 

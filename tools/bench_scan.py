@@ -24,8 +24,8 @@ def main():
                          j["value"] / 1e6, (j.get("parity") or {}).get("match"), c.get("inflight_decodes"),
                          c.get("production_streams"), c.get("segments"), c.get("hw_queues"), clk))
     out = ["# Round bench lines (builder, one MI355X per line, 20 timed steps / 5 warmup unless named)", "",
-           "Every line is `bench.py` output of the tree at that point (`gpurun_out/<run>/`; the runs' scripts are "
-           "`tools/session_*.sh`).",
+           "Every line is `bench.py` output of the tree at that point (`gpurun_out/<run>/`, run with "
+           "`tools/bench_matrix.sh`).",
            "frames/s is the whole job's, per GPU; N > 1 rows are one GPU running one rank's shard of C4's 2048 "
            "utterances.", "", "| run | what the run tested |", "|---|---|"]
     out += [f"| {k} | {v} |" for k, v in notes.items()]
