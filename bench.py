@@ -1334,7 +1334,8 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             "inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
             "decode_cus": desc["decode_cus"], "fused_emission": fused,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
-            "segments": desc.get("segments"),
+            "segments": desc.get("segments"), "drain_held_batches": desc.get("drain_held_batches"),
+            "first_segment_share": desc.get("first_segment_share"),
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],
             "stages": stages, "clock": clock_fig, "cu_placement": placement, "serialized": ser, "host": host,
             "pipeline": f"native asr_pipeline ({desc['mode']}): {desc['inflight']} decodes in flight on "

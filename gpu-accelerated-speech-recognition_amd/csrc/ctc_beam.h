@@ -46,7 +46,8 @@ struct CtcArgs {
     double* best_score;     // [B]
     uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
     uint32_t* tile0;        // [B][T][WREC] first label tile per frame (wide kernel, V > 65; NULL: in-kernel)
-    int diag;               // bit 0: the wide kernel always takes its register fallback (tests; ASR_CTC_WIDE_FALLBACK=1)
+    int diag;               // bit 0: the wide kernel always takes its register fallback (tests; ASR_CTC_WIDE_FALLBACK=1);
+                            // bit 1: its adoption list holds no hit: every adoption takes the one-thread scan (tests; ASR_CTC_WIDE_ADOPT_CAP=1)
     // Segmented decode (asr_ctc_decode_segment; one-wave kernel only): this
     // launch runs frames [t0, t1) of T, emis addresses frame t0, and the beam
     // of every unfinished utterance is saved to / restored from seg_state

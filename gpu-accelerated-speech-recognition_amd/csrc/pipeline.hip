@@ -78,6 +78,16 @@ struct asr_pipeline {
     long grows = 0;       // SHARED + fuse: input-projection rows run on the decode CUs
     int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
+    double seg0 = 0.0;    // first segment's share of T when S = 2 (0: T / 2)
+    // Drain (S > 1): the last decode segment of the newest `hold` batches is
+    // held back.  A newer batch releases the oldest onto its decode stream
+    // (the steady state); when the caller drains (collects a batch within D
+    // of a held one), every held segment is queued on its batch's production
+    // stream instead, behind that stream's last production: the drain's
+    // decodes then also use the production CUs, which are idle by then.
+    int hold = 0;
+    std::deque<long> held;
+    std::vector<hipEvent_t> ev_dpre;  // [nbuf] decode of segments [0, S - 1) of buffer k done
     int pcus = 0;         // CUs one production stream's recurrence may count on (one-launch H > 256 recurrence)
     int G = 1;            // GROUPS2: batches whose recurrences run as one (a production group)
     std::vector<long> group;          // batches whose input projection is queued, recurrence not yet
@@ -156,6 +166,15 @@ int mark(asr_pipeline* p, int which, int k, hipStream_t s) {
     return ASR_OK;
 }
 
+// First frame of T-segment s (s = S: T).
+int seg_bound(const asr_pipeline* p, int s) {
+    const int T = p->cfg.T;
+    if (s <= 0) return 0;
+    if (s >= p->S) return T;
+    if (p->S == 2 && p->seg0 > 0.0) return std::max(1, std::min(T - 1, (int)(p->seg0 * T + 0.5)));
+    return (int)((long)T * s / p->S);
+}
+
 void set_failed(asr_pipeline* p, long from, int rc) {
     if (p->fail_from < 0 || from < p->fail_from) p->fail_from = from;
     if (p->fail_rc == ASR_OK) p->fail_rc = rc;
@@ -203,7 +222,7 @@ int produce_full_segments(asr_pipeline* p, long i, const float* x, hipStream_t s
     const int k = (int)(i % p->nbuf);
     int rc = ASR_OK;
     for (int s = 0; s < p->S && !rc; s++) {
-        const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
+        const int t0 = seg_bound(p, s), t1 = seg_bound(p, s + 1);
         const long r0 = (long)t0 * c.B, rows = (long)(t1 - t0) * c.B;
         float* hs = p->hid[k] + r0 * c.H;
         rc = asr_linear_fwd(x + r0 * c.in, p->W_ih, nullptr, hs, (int)rows, c.in, c.H, ASR_EPI_NONE, sp);
@@ -263,7 +282,7 @@ int produce_fused_segments(asr_pipeline* p, long i, const float* x, hipStream_t 
     int rc = ASR_OK;
     if (frac128 > 0) ASR_HIP_TRY(hipStreamWaitEvent(p->s_gdec, p->ev_free[k], 0));
     for (int s = 0; s < p->S && !rc; s++) {
-        const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
+        const int t0 = seg_bound(p, s), t1 = seg_bound(p, s + 1);
         const long r0 = (long)t0 * c.B, rows = (long)(t1 - t0) * c.B;
         const long ga = frac128 > 0 ? std::min(rows, frac128 * rows / ((long)c.T * c.B) / 128 * 128) : 0;
         if (ga > 0) {
@@ -368,6 +387,37 @@ int produce_tail(asr_pipeline* p, long i) {
     return ASR_OK;
 }
 
+// Queue the held last decode segment of batch i: on its decode stream, or
+// (drain) on its production stream behind that stream's productions, after
+// the decode of its earlier segments.
+int release_held(asr_pipeline* p, long i, bool drain) {
+    const auto& c = p->cfg;
+    const int k = (int)(i % p->nbuf);
+    const int s = p->S - 1;
+    const int t0 = seg_bound(p, s);
+    hipStream_t st = drain ? p->s_prod[i % p->P] : p->s_dec[i % p->D];
+    if (drain) ASR_HIP_TRY(hipStreamWaitEvent(st, p->ev_dpre[k], 0));
+    ASR_HIP_TRY(hipStreamWaitEvent(st, p->ev_seg[(size_t)k * p->S + s], 0));
+    int rc = asr_ctc_decode_segment(p->dec[k], p->emis[k] + (long)t0 * c.B * c.V, c.T, t0, c.T, c.B,
+                                    (long)c.B * c.V, c.V, nullptr, 1, st);
+    if (rc) return rc;
+    if (int r = mark(p, 3, k, st)) return r;
+    ASR_HIP_TRY(hipEventRecord(p->ev_free[k], st));
+    return ASR_OK;
+}
+
+// Every held segment onto the production streams (the caller drains).
+int release_all_held(asr_pipeline* p) {
+    int rc = ASR_OK;
+    while (!p->held.empty() && !rc) {
+        const long h = p->held.front();
+        p->held.pop_front();
+        rc = release_held(p, h, true);
+        if (rc) set_failed(p, h, rc);   // batch h was accepted: its results can never come
+    }
+    return rc;
+}
+
 int enqueue_decode(asr_pipeline* p, long i) {
     const auto& c = p->cfg;
     const int k = (int)(i % p->nbuf);
@@ -375,12 +425,25 @@ int enqueue_decode(asr_pipeline* p, long i) {
     if (fault(p, i, "decode")) return ASR_ERR_INTERNAL;
     int rc = ASR_OK;
     if (p->S > 1) {   // segment by segment, each behind its production
-        for (int s = 0; s < p->S && !rc; s++) {
-            const int t0 = (int)((long)c.T * s / p->S), t1 = (int)((long)c.T * (s + 1) / p->S);
+        const int ns = p->hold > 0 ? p->S - 1 : p->S;   // held: the last one is queued later
+        for (int s = 0; s < ns && !rc; s++) {
+            const int t0 = seg_bound(p, s), t1 = seg_bound(p, s + 1);
             ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_seg[(size_t)k * p->S + s], 0));
             if (s == 0) if (int r = mark(p, 2, k, sd)) return r;
             rc = asr_ctc_decode_segment(p->dec[k], p->emis[k] + (long)t0 * c.B * c.V, c.T, t0, t1, c.B,
                                         (long)c.B * c.V, c.V, nullptr, 1, sd);
+        }
+        if (rc) return rc;
+        if (ns < p->S) {
+            ASR_HIP_TRY(hipEventRecord(p->ev_dpre[k], sd));
+            p->held.push_back(i);
+            p->decoded = i + 1;
+            while ((int)p->held.size() > p->hold) {   // the steady state: on its own decode stream
+                const long h = p->held.front();
+                p->held.pop_front();
+                if (int r = release_held(p, h, false)) return r;
+            }
+            return ASR_OK;
         }
     } else {
         ASR_HIP_TRY(hipStreamWaitEvent(sd, p->ev_ready[k], 0));
@@ -470,6 +533,10 @@ int fetch_to(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, do
     // caller reaches it (C2, 20 steps: the last decode started 1.5 ms late,
     // 8 % of the job).  In steady state the caller fetches batches more than
     // D behind the newest, so nothing changes there.
+    if (!p->held.empty() && j + p->D >= p->held.front()) {   // draining: held segments on the production CUs
+        const int rc = release_all_held(p);
+        if (rc && (p->fail_from >= 0 && j >= p->fail_from)) return rc;
+    }
     const bool drain_tail = p->pending_tail >= 0 && j + p->D >= p->pending_tail;
     const bool drain_group = !p->group.empty() && j + p->D >= p->group.front();
     if (j >= p->decoded || drain_tail || drain_group) {
@@ -521,6 +588,7 @@ void release(asr_pipeline* p) {
     for (auto b : p->emis) hipFree(b);
     for (auto b : p->hst) hipFree(b);
     for (auto e : p->ev_seg) if (e) hipEventDestroy(e);
+    for (auto e : p->ev_dpre) if (e) hipEventDestroy(e);
     for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec, &p->ev_t[0], &p->ev_t[1], &p->ev_t[2],
                     &p->ev_t[3]})
         for (auto e : *v) if (e) hipEventDestroy(e);
@@ -817,6 +885,14 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         p->tail_own = p->split && nstreams() < p->hw_queues;
         p->streams = nstreams() + (p->tail_own ? 1 : 0);
     }
+    // drain hold (S > 1; A/B: ASR_PIPELINE_DRAIN=W held batches, -1: P - 1)
+    // and the first segment's share of T (ASR_PIPELINE_SEG0, S = 2)
+    if (p->S > 1) {
+        const char* de = getenv("ASR_PIPELINE_DRAIN");
+        const int w = de ? atoi(de) : 0;
+        p->hold = std::max(0, w < 0 ? p->P - 1 : std::min(w, p->P - 1));
+        if (const char* f0 = getenv("ASR_PIPELINE_SEG0")) p->seg0 = std::max(0.0, std::min(0.95, atof(f0)));
+    }
     // CU groups (GROUPS / GROUPS2), from the decode count the queue fit left:
     // decode d runs on group d % ngroups, so an explicit inflight beyond the
     // groups queues decodes behind a group's current one.  Not the default:
@@ -880,6 +956,9 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
                 if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;
                 p->ev_seg.push_back(e);
             }
+            hipEvent_t e = nullptr;
+            if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;
+            p->ev_dpre.push_back(e);
         }
         // the decoders' schedule (asr_ctc_set_concurrency): D batches share the
         // decode CUs, which are dcus of the ncu the decoder plans for
@@ -1037,6 +1116,13 @@ int asr_pipeline_get_groups(asr_pipeline_t* p, int* group) {
 int asr_pipeline_get_segments(asr_pipeline_t* p, int* segments) {
     if (!p || !segments) return ASR_ERR_ARG;
     *segments = p->S;
+    return ASR_OK;
+}
+
+int asr_pipeline_get_drain(asr_pipeline_t* p, int* held_batches, double* first_segment_share) {
+    if (!p) return ASR_ERR_ARG;
+    if (held_batches) *held_batches = p->hold;
+    if (first_segment_share) *first_segment_share = p->S > 1 ? (double)seg_bound(p, 1) / p->cfg.T : 1.0;
     return ASR_OK;
 }
 

@@ -495,7 +495,7 @@ struct asr_ctc {
     uint64_t* d_fin_ts = nullptr;    // [B][kcap][2] append frames of the final tails
     uint32_t* d_tile0 = nullptr;     // [B][T] first label tile per frame (wide kernel, V > 65)
     bool tile0 = true;               // precompute first tiles (ASR_CTC_TILE0=0: in-kernel, for A/B timing)
-    int diag = 0;                    // CtcArgs::diag (ASR_CTC_WIDE_FALLBACK=1: bit 0)
+    int diag = 0;                    // CtcArgs::diag (ASR_CTC_WIDE_FALLBACK=1: bit 0, ASR_CTC_WIDE_ADOPT_CAP=1: bit 1)
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
     unsigned char* h_res = nullptr;   // pinned mirror of d_res
@@ -735,6 +735,10 @@ int asr_ctc_create(const int32_t* codes, int V, int beam_width, int blank_id, in
     if (const char* w = getenv("ASR_CTC_WAVES")) h->waves_override = atoi(w);
     if (const char* t0 = getenv("ASR_CTC_TILE0")) h->tile0 = atoi(t0) != 0;
     if (const char* fb = getenv("ASR_CTC_WIDE_FALLBACK")) h->diag = atoi(fb) != 0 ? 1 : 0;
+    // ASR_CTC_WIDE_ADOPT_CAP=1 (tests): the wide kernel lists no orphan-filter
+    // hit for the block-wide adoption scan: every hit takes the one-thread
+    // scan (the path past 128 hits per frame)
+    if (const char* ac = getenv("ASR_CTC_WIDE_ADOPT_CAP")) h->diag |= atoi(ac) != 0 ? 2 : 0;
     if (asr::ctc_lds_bytes(plan(h, 8)) > 160 * 1024) { delete h; return ASR_ERR_UNSUPPORTED; }
     int rc = asr::ctc_set_max_lds();
     if (rc) { delete h; return rc; }

@@ -397,6 +397,14 @@ int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
  * H > 256: one per-frame step launch for G batches; a batch's production
  * then starts when its group is complete or its results are asked for). */
 int asr_pipeline_get_segments(asr_pipeline_t* p, int* segments);
+/* The drain schedule (T-segmented batches): the last decode segment of the
+ * newest `held_batches` batches is held back; a newer batch releases the
+ * oldest onto its decode stream, and when the caller drains (collects a
+ * batch within `inflight` of a held one) every held segment is queued on its
+ * batch's production stream behind that stream's last production, so the
+ * drain's decodes also use the production CUs.  first_segment_share: the
+ * first T-segment's share of T (0.5 = equal halves).  Either may be NULL. */
+int asr_pipeline_get_drain(asr_pipeline_t* p, int* held_batches, double* first_segment_share);
 int asr_pipeline_get_groups(asr_pipeline_t* p, int* group);
 int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod_streams, int* decode_cus,
                           int* decode_waves);

@@ -273,3 +273,72 @@ def test_c4_pipeline_full_size_vs_oracle(B):
     for i, u in enumerate(sub):
         assert labels[u] == [int(c) for c in ref[i][0][0]], f"utterance {u}: best labels differ from the oracle"
         assert abs(lp[u] - ref[i][0][1]) <= 1e-9 * max(1.0, abs(ref[i][0][1])), (u, lp[u], ref[i][0][1])
+
+
+C5P = GOLDEN / "c5_production.json"
+
+
+@pytest.mark.skipif(not C5P.exists(), reason="tests/golden/c5_production.json not generated")
+def test_c5_production_full_length_vs_oracle(monkeypatch):
+    """C5 at its full length on PRODUCTION emissions: the
+    bench's C5 model (H = 1024, V = 1000, 32 utterances, T = 2000) through the
+    library's fp32 dense arithmetic, log_softmax emissions — where the wide
+    kernel's orphan adoption fires (~0.1-0.2 per frame) — against the CPU
+    oracle's decode of the same bytes (tests/golden/c5_production.json,
+    written in the dev container by tests/golden/make_c5_production_golden.py
+    from tools/dump_c5_emissions.py's dump; the emission digests tie the
+    fixture to these bytes).  Four utterances x 2000 frames:
+      * the wide kernel, whole decode: best labels, beam size, ranked labels
+        (digest) and every rank's log-prob within 1e-9 relative;
+      * the same in two T-segments (the C5 pipeline's hand-off), bit for bit;
+      * with every orphan adoption forced through the one-thread scan that
+        runs past 128 filter hits per frame (ASR_CTC_WIDE_ADOPT_CAP=1), bit
+        for bit;
+      * the four rows inside the whole 32-utterance batch, bit for bit."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import dump_c5_emissions as c5
+    g = json.loads(C5P.read_text())
+    e, em = c5.production_emissions(asr)
+    T, B, V, beam = g["T"], g["B"], g["V"], g["beam"]
+    assert e.shape == (T, B, V)
+    uids = g["utterances"]
+    for u, d in zip(uids, g["emis_sha256"]):
+        assert c5.digest(e[:, u, :]) == d, f"utterance {u}: emissions differ from the fixture's (regenerate it)"
+    sub = np.ascontiguousarray(e[:, uids, :])
+    d_sub = asr.DeviceMatrix.from_numpy(sub.reshape(T * len(uids), V))
+
+    def run(segments):
+        d = asr.CTCDecoder(V, beam, 0)
+        n = len(uids)
+        if segments:
+            for t0, t1 in ((0, 1111), (1111, T)):
+                d.decode_segment(d_sub.ptr + 4 * t0 * n * V, T, t0, t1, n, True)
+        else:
+            d.decode_device(d_sub.ptr, T, n, True)
+        assert d.config()[1] == 8   # the wide kernel
+        beams = d.beams(max_hyps=d.config()[0])
+        d.close()
+        return beams
+
+    whole = run(False)
+    for i, u in enumerate(uids):
+        got = whole[i]
+        assert got[0][0] == g["best_labels"][i], f"utterance {u}: best differs from the oracle"
+        assert len(got) == g["n_hyps"][i], f"utterance {u}: beam size differs"
+        assert labels_digest(got) == g["beam_labels_sha256"][i], f"utterance {u}: ranked beam differs"
+        for (_, x), y in zip(got, g["beam_logp"][i]):
+            assert abs(x - y) <= 1e-9 * max(1.0, abs(y)), f"utterance {u}: {x} vs {y}"
+
+    def same(a, what):
+        for i in range(len(uids)):
+            assert [l for l, _ in a[i]] == [l for l, _ in whole[i]], f"{what}: utterance {uids[i]} labels"
+            assert [s for _, s in a[i]] == [s for _, s in whole[i]], f"{what}: utterance {uids[i]} scores"
+
+    same(run(True), "two T-segments")
+    monkeypatch.setenv("ASR_CTC_WIDE_ADOPT_CAP", "1")
+    same(run(False), "adoptions through the one-thread scan")
+    monkeypatch.delenv("ASR_CTC_WIDE_ADOPT_CAP")
+    dec, best = decode_best(em.ptr, T, B, V, beam, True)
+    dec.close()
+    for i, u in enumerate(uids):
+        assert best[0][u] == whole[i][0][0] and best[1][u] == whole[i][0][1], f"utterance {u} in the batch"

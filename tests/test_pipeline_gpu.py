@@ -245,6 +245,50 @@ def test_pipeline_persistent_recurrence_fault_recovers(monkeypatch):
         assert g[0] == ref[0] and np.array_equal(g[1], ref[1])
 
 
+@pytest.mark.parametrize("drain,seg0,B", [("-1", "", 300), ("-1", "0.3", 300), ("2", "0.25", 600), ("", "0.4", 256)])
+def test_pipeline_drain_schedule(drain, seg0, B, monkeypatch):
+    """The drain schedule (ASR_PIPELINE_DRAIN: the last decode segment of the
+    newest batches held back, released onto its decode stream by newer
+    batches or onto its production stream when the caller drains) and an
+    uneven first T-segment (ASR_PIPELINE_SEG0) only move work between streams
+    and CUs: every batch equals the sequential fused production + whole
+    decode, with submits ahead of collects, interleaved, and a drain in the
+    middle (collect everything, then submit more)."""
+    if drain:
+        monkeypatch.setenv("ASR_PIPELINE_DRAIN", drain)
+    if seg0:
+        monkeypatch.setenv("ASR_PIPELINE_SEG0", seg0)
+    T, inp, H, V, beam = 41, 48, 64, 29, 40
+    W = _weights(inp, H, V, seed=B + 3)
+    rng = np.random.default_rng(B)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(3)]
+    p = asr.Pipeline(T, B, inp, H, V, beam, W, segments=2)
+    d = p.describe()
+    assert d["mode"] == "chip-filling batches" and d["segments"] == 2, d
+    order = [0, 1, 2, 0, 1, 2, 0, 1, 2, 0, 1, 2]
+    got = []
+
+    def take():
+        lab, ln, lp, _ = p.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+
+    for i in order[:9]:   # a ring's worth ahead, then collects interleaved
+        p.submit(xs[i])
+        if p.pending() > 6:
+            take()
+    while p.pending():    # the caller drains
+        take()
+    for i in order[9:]:   # and the pipeline goes on
+        p.submit(xs[i])
+    while p.pending():
+        take()
+    p.close()
+    assert len(got) == len(order)
+    refs = [_sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True) for x in xs]
+    for g, i in zip(got, order):
+        assert g[0] == refs[i][0] and np.array_equal(g[1], refs[i][1]), f"input {i}"
+
+
 @pytest.mark.parametrize("group", ["2", "3"])
 def test_pipeline_production_groups(group, monkeypatch):
     """H > 256 (C5-like): the recurrences of G consecutive batches run as one

@@ -7,7 +7,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 P=$R/gpu-accelerated-speech-recognition_amd
 T=$(mktemp -d)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -mcode-object-version=5 -O3 -std=c++17 -ffp-contract=off \
-    -I$R/include -I$P/csrc --cuda-device-only -c "$P/$1" -o $T/b.co
+    -I$R/include -I$P/csrc ${KR_FLAGS:-} --cuda-device-only -c "$P/$1" -o $T/b.co
 /opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input=$T/b.co \
     --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=$T/d.o
 /opt/rocm/lib/llvm/bin/llvm-readelf --notes $T/d.o | \
