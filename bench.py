@@ -53,21 +53,18 @@ from pathlib import Path
 
 import numpy as np
 
-# One hardware queue per HIP stream: D decode streams + the recurrence and
-# GEMM streams of production exceed HIP's default of 4, and streams sharing a
-# queue run one after another (C5 with 5 streams on 4 queues: 1.03 M vs
-# 3.48 M frames/s, gpurun_out/r2g31).  Read when the HIP runtime starts.
-# Small shards (C4 at N = 8: 256 utterances per GPU) keep 8 decodes and 8
-# productions in flight: 17 streams.
-# --hw-queues N (read here, before the HIP runtime starts) measures the
-# library at another queue count, e.g. HIP's default 4.
+# Hardware queues: HIP maps the UNMASKED streams of a process round-robin
+# onto GPU_MAX_HW_QUEUES queues (default 4, read when the runtime starts);
+# the pipeline's CU-masked decode and production streams get queues of
+# their own, so the bench runs at whatever the environment sets — HIP's
+# default unless exported (round 6: the same frames/s at 4 and 24 queues,
+# DESIGN.md §11).  --hw-queues N (read here, before the HIP runtime starts)
+# measures another count.
 _hwq = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--hw-queues=")), None)
 if _hwq is None and "--hw-queues" in sys.argv[:-1]:
     _hwq = sys.argv[sys.argv.index("--hw-queues") + 1]
 if _hwq is not None:
     os.environ["GPU_MAX_HW_QUEUES"] = str(int(_hwq))
-elif int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
-    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 # c10's INFO lines (gloo's "[Gloo] Rank r is connected to n peer ranks") can
 # land on stdout before rank 0's JSON line: keep stdout to that one line.
@@ -544,7 +541,7 @@ def launch_ranks(n: int) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hw-queues", type=int, default=None,
-                    help="GPU_MAX_HW_QUEUES for this run (default 24; the library fits its schedule to it)")
+                    help="GPU_MAX_HW_QUEUES for this run (default: the environment's, HIP's 4 if unset; the library fits its unmasked streams to it)")
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); started by this script when WORLD_SIZE is unset")
     ap.add_argument("--steps", type=int, default=20)
@@ -1334,6 +1331,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
             "inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
             "decode_cus": desc["decode_cus"], "fused_emission": fused,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],
+            "shared_queue_streams": desc.get("shared_queue_streams"),
             "segments": desc.get("segments"), "drain_held_batches": desc.get("drain_held_batches"),
             "first_segment_share": desc.get("first_segment_share"),
             "decode_cu_gemm_rows": desc["decode_cu_gemm_rows"],

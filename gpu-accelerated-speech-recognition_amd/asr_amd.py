@@ -58,7 +58,7 @@ EXPORTS = [
     "asr_ctc_set_concurrency", "asr_rnn_set_recurrence", "asr_rnn_get_recurrence",
     "asr_set_dense_arith", "asr_get_dense_arith",
     "asr_pipeline_create", "asr_pipeline_submit", "asr_pipeline_collect", "asr_pipeline_pending",
-    "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams",
+    "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams", "asr_pipeline_get_queue_use",
     "asr_pipeline_peek_emissions", "asr_pipeline_get_segments", "asr_pipeline_get_drain", "asr_pipeline_get_groups",
     "asr_pipeline_get_placement", "asr_pipeline_probe_placement", "asr_pipeline_set_timing",
     "asr_pipeline_get_timeline", "asr_pipeline_destroy",
@@ -133,6 +133,7 @@ def lib() -> ctypes.CDLL:
         "asr_pipeline_get_production": [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_longlong),
                                         ctypes.POINTER(_i)],
         "asr_pipeline_get_streams": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)],
+        "asr_pipeline_get_queue_use": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_pipeline_get_placement": [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
                                        ctypes.POINTER(_i)],
         "asr_pipeline_probe_placement": [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)],
@@ -642,13 +643,17 @@ class Pipeline:
         check(lib().asr_pipeline_get_streams(self.h, ctypes.byref(ns), ctypes.byref(hq)), "asr_pipeline_get_streams")
         check(lib().asr_pipeline_get_segments(self.h, ctypes.byref(sg)), "asr_pipeline_get_segments")
         check(lib().asr_pipeline_get_groups(self.h, ctypes.byref(gp)), "asr_pipeline_get_groups")
+        qs, qd = _i(), _i()
+        check(lib().asr_pipeline_get_queue_use(self.h, ctypes.byref(qs), ctypes.byref(qd)),
+              "asr_pipeline_get_queue_use")
         hb, f0 = _i(), ctypes.c_double()
         check(lib().asr_pipeline_get_drain(self.h, ctypes.byref(hb), ctypes.byref(f0)), "asr_pipeline_get_drain")
         return {"mode": PIPELINE_MODES.get(m.value, m.value), "inflight": d.value, "prod_streams": p.value,
                 "decode_cus": c.value, "decode_waves": w.value, "fused_emission": bool(fz.value),
                 "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
                 "hw_queues": hq.value, "segments": sg.value, "groups": gp.value,
-                "drain_held_batches": hb.value, "first_segment_share": round(f0.value, 4)}
+                "drain_held_batches": hb.value, "first_segment_share": round(f0.value, 4),
+                "shared_queue_streams": qs.value, "dedicated_queue_streams": qd.value}
 
     def placement(self):
         """[(role name, cu_lo, cu_hi)] of every stream the pipeline created."""

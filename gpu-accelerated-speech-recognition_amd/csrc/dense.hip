@@ -461,7 +461,10 @@ int gemm_launch(const GemmArgs& g, int epi, hipStream_t s) {
     // fp32-accurate split-bf16 kernel (dense_x3.hip) for the shapes it takes;
     // the pipeline's short-workgroup request (asr_internal_gemm_tiled) runs it
     // in runs of that many row tiles instead of persistent workgroups
-    if (dense_x3_on() && gemm_x3_applies(g, epi)) return gemm_x3_launch(g, epi, asr_internal_gemm_tiled, s);
+    if (dense_x3_on() && gemm_x3_applies(g, epi)) {
+        const int rc = gemm_x3_launch(g, epi, asr_internal_gemm_tiled, s);
+        if (rc != ASR_ERR_UNSUPPORTED) return rc;   // (K > 256 under stream capture: the fp32 kernels)
+    }
     if (epi == EPI_LOGSOFTMAX && g.N > 64) {
         // Rows wider than one workgroup tile (e.g. C5's V = 1000): bias GEMM,
         // then a row-wise log_softmax pass in place (model.py:49).

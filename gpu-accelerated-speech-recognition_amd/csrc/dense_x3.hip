@@ -22,6 +22,7 @@
 #include "dense.h"
 
 #include <atomic>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 
@@ -370,11 +371,269 @@ static int launch_gemm_x3_epi(const GemmArgs& g, int tpw, hipStream_t s) {
     return launch_gemm_x3_k<8, EPI>(g, tpw, s);
 }
 
+// ---------------------------------------------------------------------------
+// GEMM C = A.B (+ bias, ReLU) on the split arithmetic for K > 256 (C5's
+// input projection [T*B, 1024] x [1024, 1024] and emission layer [T*B, 1024]
+// x [1024, 1000]; BL's K = 2048), where the K <= 256 kernel's B-in-registers
+// scheme cannot hold B.  Round 6.
+//   * B is split ONCE per call into its three pieces, stored fragment-major
+//     (x3k_split_b_kernel: for 32-k chunk c and 16-column tile nt, the 64
+//     lanes' 16-byte MFMA B fragments are one contiguous KiB), into a
+//     stream-ordered scratch allocation, so the GEMM moves B with
+//     global_load_lds (LDS-DMA: a KiB per wave-instruction, no registers)
+//     and never splits it again;
+//   * 128 x 128 output tiles, 8 waves (4 x 2), each wave 32 x 64: per 32-k
+//     chunk 2 x 4 tiles x 6 products = 48 v_mfma_f32_16x16x32_bf16;
+//   * A (fp32) is loaded into registers one chunk ahead, split, and written
+//     fragment-major into LDS (conflict-free ds_read_b128 fragment reads);
+//     LDS double-buffered, one barrier per chunk;
+//   * the six products per tile in the K <= 256 kernel's order (ascending
+//     magnitude), chunks in k order: fp32-accurate, and a row's bits depend
+//     on the shape only (never on M: utterance sharding relies on that).
+// Workgroups map to tiles XCD-aware: the 8 column tiles of a row block run
+// on one XCD (its L2 keeps the A rows they share).
+// ---------------------------------------------------------------------------
+constexpr int XK_BM = 128, XK_BN = 128;
+constexpr int XK_WAVES = 8;
+constexpr int XK_RT = XK_BM / 16, XK_CT = XK_BN / 16;    // 16-row / 16-column tiles per workgroup tile
+constexpr int XK_FRAG = 512;                             // bf16 per fragment block (64 lanes x 8)
+constexpr int XK_ASTAGE = 3 * XK_RT * XK_FRAG;           // bf16 of one A stage (three pieces)
+constexpr int XK_BSTAGE = 3 * XK_CT * XK_FRAG;           // bf16 of one B stage
+constexpr int XK_LDS = 2 * (XK_ASTAGE + XK_BSTAGE) * 2;  // bytes, double-buffered
+
+// B (k, n) = B[k * sbk + n * sbn] -> Bf[p][c][nt][lane][8]: lane l = 16 gq + c15
+// holds n = 16 nt + c15, k = 32 c + 8 gq + j; zero past K and N.  nct: column
+// tiles stored (a multiple of XK_CT).
+__global__ __launch_bounds__(256) void x3k_split_b_kernel(const float* __restrict__ Bm, long sbk, long sbn, int K,
+                                                          int N, int nch, int nct, __bf16* __restrict__ Bf) {
+    const long f = (long)blockIdx.x * 256 + threadIdx.x;   // one lane-fragment per thread
+    const long nfrag = (long)nch * nct * 64;
+    if (f >= nfrag) return;
+    const int l = (int)(f & 63), nt = (int)((f >> 6) % nct), c = (int)(f / (64L * nct));
+    const int gq = l >> 4, c15 = l & 15;
+    const int n = 16 * nt + c15;
+    bf16x8 ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int k = 32 * c + 8 * gq + j;
+        const float b = (k < K && n < N) ? Bm[(long)k * sbk + (long)n * sbn] : 0.f;
+        __bf16 h, m, lo;
+        split3(b, h, m, lo);
+        ph[j] = h;
+        pm[j] = m;
+        pl[j] = lo;
+    }
+    const long piece = (long)nch * nct * XK_FRAG;
+    bf16x8* dst = reinterpret_cast<bf16x8*>(Bf + ((long)c * nct + nt) * XK_FRAG) + l;
+    dst[0] = ph;
+    dst[piece / 8] = pm;
+    dst[2 * piece / 8] = pl;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(64 * XK_WAVES) void gemm_x3k_kernel(GemmArgs g, const __bf16* __restrict__ Bf,
+                                                                 int nch, int nct, int nrt_tiles) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 xks[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;   // wave rows 32 wm .., columns 64 wn ..
+    // XCD-aware tile order: consecutive tiles (the column tiles of one row
+    // block) on one XCD (workgroups are dealt to the 8 XCDs round-robin)
+    const int nwg = gridDim.x;
+    const int id = blockIdx.x;
+    const int per = nwg / 8;
+    const int lin = (id < per * 8) ? (id & 7) * per + (id >> 3) : id;
+    const int nctile = nct / XK_CT;
+    const int mt = lin / nctile, ntile = lin - mt * nctile;
+    if (mt >= nrt_tiles) return;
+    const long r0 = (long)mt * XK_BM;
+    const int n0 = ntile * XK_BN;
+    const long rows = min((long)XK_BM, (long)g.M - r0);
+    const auto rsA = brsrc(g.A + r0 * g.sam, rows * g.sam * 4);
+    const long piece = (long)nch * nct * XK_FRAG;
+    // A staging: 128 rows x 32 k per chunk = 1024 float4, two per thread
+    f32x4 st[2];
+    auto load_a = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int idx = tid + 512 * i;
+            const int row = idx >> 3, kq = idx & 7;
+            const int k = 32 * c + 4 * kq;
+            f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rsA, (row * (int)g.sam + k) * 4, 0, 0));
+            if (k >= g.K) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            st[i] = v;
+        }
+    };
+    auto stage_a = [&](int buf) {
+        __bf16* base = xks + buf * (XK_ASTAGE + XK_BSTAGE);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int idx = tid + 512 * i;
+            const int row = idx >> 3, kq = idx & 7;
+            const int rt = row >> 4, c15 = row & 15, gq = kq >> 1, half = kq & 1;
+            bf16x4 h, m, l;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                __bf16 a, b, cc;
+                split3(st[i][e], a, b, cc);
+                h[e] = a;
+                m[e] = b;
+                l[e] = cc;
+            }
+            __bf16* p = base + (rt * 64 + gq * 16 + c15) * 8 + half * 4;
+            *reinterpret_cast<bf16x4*>(p) = h;
+            *reinterpret_cast<bf16x4*>(p + XK_RT * XK_FRAG) = m;
+            *reinterpret_cast<bf16x4*>(p + 2 * XK_RT * XK_FRAG) = l;
+        }
+    };
+    // B stage: 3 pieces x XK_CT column tiles = 24 fragment blocks of 1 KiB,
+    // three per wave, by LDS-DMA
+    auto load_b = [&](int c, int buf) {
+        __bf16* base = xks + buf * (XK_ASTAGE + XK_BSTAGE) + XK_ASTAGE;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const int blk = w * 3 + q;              // 0 .. 23
+            const int p = blk / XK_CT, ctl = blk - p * XK_CT;
+            const __bf16* src = Bf + p * piece + ((long)c * nct + (n0 >> 4) + ctl) * XK_FRAG + lane * 8;
+            __builtin_amdgcn_global_load_lds(const_cast<__bf16*>(src),
+                                             (__attribute__((address_space(3))) void*)(base + blk * XK_FRAG), 16, 0,
+                                             0);
+        }
+    };
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load_a(0);
+    load_b(0, 0);
+    stage_a(0);
+    if (nch > 1) load_a(1);
+    __syncthreads();
+    int cur = 0;
+    for (int c = 0; c < nch; c++) {
+        if (c + 1 < nch) load_b(c + 1, cur ^ 1);
+        const __bf16* ab = xks + cur * (XK_ASTAGE + XK_BSTAGE);
+        const __bf16* bb = ab + XK_ASTAGE;
+        bf16x8 fa[2][3], fb[4][3];
+#pragma unroll
+        for (int rt = 0; rt < 2; rt++)
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                fa[rt][p] = *reinterpret_cast<const bf16x8*>(ab + ((p * XK_RT + 2 * wm + rt) * 64 + lane) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                fb[ct][p] = *reinterpret_cast<const bf16x8*>(bb + ((p * XK_CT + 4 * wn + ct) * 64 + lane) * 8);
+#pragma unroll
+        for (int rt = 0; rt < 2; rt++) {
+            // the six piece products in ascending order of magnitude (X3_PRODUCTS)
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt][2], fb[ct][0], acc[rt][ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt][1], fb[ct][1], acc[rt][ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt][0], fb[ct][2], acc[rt][ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt][1], fb[ct][0], acc[rt][ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt][0], fb[ct][1], acc[rt][ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt][0], fb[ct][0], acc[rt][ct], 0, 0, 0);
+        }
+        if (c + 1 < nch) {
+            stage_a(cur ^ 1);
+            if (c + 2 < nch) load_a(c + 2);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    // epilogue: lane (gq, c15) of tile (rt, ct) holds rows 4 gq + j, column c15
+    const int gq = lane >> 4, c15 = lane & 15;
+    const auto cs = brsrc(g.C + r0 * g.ldc, rows * g.ldc * 4);
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) {
+        const int n = n0 + 64 * wn + 16 * ct + c15;
+        if (n >= g.N) continue;
+        float bias = 0.f;
+        if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bias = g.b1[n];
+#pragma unroll
+        for (int rt = 0; rt < 2; rt++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float y = acc[rt][ct][j];
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) y = y + bias;
+                if (EPI == EPI_BIAS_RELU && y < 0.f) y = 0.f;
+                bstore(cs, ((32 * wm + 16 * rt + 4 * gq + j) * (int)g.ldc + n) * 4, y);
+            }
+    }
+}
+
+static int x3k_pool_once() {   // keep freed scratch in the pool (no release at each sync)
+    static std::mutex mu;
+    static uint64_t done = 0;
+    int dev = 0;
+    ASR_HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    if (dev >= 0 && dev < 64 && !(done & (1ull << dev))) {
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t thr = ~0ull;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+        done |= 1ull << dev;
+    }
+    return ASR_OK;
+}
+
+template <int EPI>
+static int launch_gemm_x3k(const GemmArgs& g, hipStream_t s) {
+    static AsrAttrOnce attr;
+    if (int r_ = attr.set((const void*)gemm_x3k_kernel<EPI>, XK_LDS)) return r_;
+    if (int r_ = x3k_pool_once()) return r_;
+    const int nch = (g.K + 31) / 32;
+    const int nct = (g.N + XK_BN - 1) / XK_BN * XK_CT;
+    const size_t bytes = (size_t)3 * nch * nct * XK_FRAG * sizeof(__bf16);
+    void* ws = nullptr;
+    ASR_HIP_TRY(hipMallocAsync(&ws, bytes, s));
+    __bf16* Bf = static_cast<__bf16*>(ws);
+    const long nfrag = (long)nch * nct * 64;
+    hipLaunchKernelGGL(x3k_split_b_kernel, dim3((unsigned)((nfrag + 255) / 256)), dim3(256), 0, s, g.B, g.sbk, g.sbn,
+                       g.K, g.N, nch, nct, Bf);
+    int rc = ASR_OK;
+    if (hipGetLastError() != hipSuccess) rc = ASR_ERR_HIP;
+    const int nrt = (int)((g.M + XK_BM - 1) / XK_BM);
+    const long nwg = (long)nrt * (nct / XK_CT);
+    if (!rc) {
+        hipLaunchKernelGGL((gemm_x3k_kernel<EPI>), dim3((unsigned)nwg), dim3(64 * XK_WAVES), XK_LDS, s, g, Bf, nch,
+                           nct, nrt);
+        if (hipGetLastError() != hipSuccess) rc = ASR_ERR_HIP;
+    }
+    ASR_HIP_TRY(hipFreeAsync(ws, s));
+    return rc;
+}
+
+// The large-K kernel (K > 256): N >= 64, and the 32-bit buffer offsets of a
+// 128-row tile and of the B scratch fit.
+static bool x3k_applies(const GemmArgs& g) {
+    const long nct = (g.N + XK_BN - 1) / XK_BN * XK_CT;
+    return g.K > 256 && g.N >= 64 && (long)g.sam * 4 * XK_BM < 0x7fffffffL &&
+           (long)g.ldc * 4 * XK_BM < 0x7fffffffL && (long)g.M / XK_BM * (nct / XK_CT) < 0x7fffffffL;
+}
+
 bool gemm_x3_applies(const GemmArgs& g, int epi) {
     if (epi != EPI_NONE && epi != EPI_BIAS && epi != EPI_BIAS_RELU) return false;
     const bool va = g.sak == 1 && (g.K % 4) == 0 && (g.sam % 4) == 0 && ((uintptr_t)g.A % 16) == 0;
-    return va && g.K <= 256 && g.N >= 64 && (long)g.sam * 4 * X3_ROWS < 0x7fffffffL &&
-           (long)g.ldc * 4 * X3_ROWS < 0x7fffffffL;
+    if (!va) return false;
+    if (g.K > 256) return x3k_applies(g);
+    return g.N >= 64 && (long)g.sam * 4 * X3_ROWS < 0x7fffffffL && (long)g.ldc * 4 * X3_ROWS < 0x7fffffffL;
 }
 
 int gemm_x3_frag_launch(const float* A, const float* W, float* P, int M, int K, int H, int tpw, hipStream_t s) {
@@ -382,7 +641,7 @@ int gemm_x3_frag_launch(const float* A, const float* W, float* P, int M, int K, 
     g.A = A; g.B = W; g.C = P;
     g.M = M; g.N = H; g.K = K;
     g.sam = K; g.sak = 1; g.sbk = H; g.sbn = 1; g.ldc = H;
-    if (!gemm_x3_applies(g, EPI_NONE) || (M % X3_ROWS) != 0 || (H % 32) != 0 || H > X3_NCOL ||
+    if (K > 256 || !gemm_x3_applies(g, EPI_NONE) || (M % X3_ROWS) != 0 || (H % 32) != 0 || H > X3_NCOL ||
         ((uintptr_t)P % 16) != 0)
         return ASR_ERR_UNSUPPORTED;
     return launch_gemm_x3_epi<X3_EPI_FRAG>(g, tpw, s);
@@ -390,6 +649,17 @@ int gemm_x3_frag_launch(const float* A, const float* W, float* P, int M, int K, 
 
 int gemm_x3_launch(const GemmArgs& g, int epi, int tpw, hipStream_t s) {
     if (!gemm_x3_applies(g, epi)) return ASR_ERR_UNSUPPORTED;
+    if (g.K > 256) {
+        // the B scratch is a stream-ordered allocation: not inside a capture
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
+            return ASR_ERR_UNSUPPORTED;
+        switch (epi) {
+            case EPI_NONE: return launch_gemm_x3k<EPI_NONE>(g, s);
+            case EPI_BIAS: return launch_gemm_x3k<EPI_BIAS>(g, s);
+            default: return launch_gemm_x3k<EPI_BIAS_RELU>(g, s);
+        }
+    }
     switch (epi) {
         case EPI_NONE: return launch_gemm_x3_epi<EPI_NONE>(g, tpw, s);
         case EPI_BIAS: return launch_gemm_x3_epi<EPI_BIAS>(g, tpw, s);

@@ -116,6 +116,7 @@ struct asr_pipeline {
     long fail_from = -1;
     int fail_rc = ASR_OK;
     int hw_queues = 4, streams = 0;   // HIP hardware queues of the process, streams created
+    int shared_queue_streams = 0;     // ... of which unmasked (they share the hw_queues)
     // every stream created: role (ASR_PIPE_ROLE_*) and CU range [lo, hi) of its mask
     struct Placed { int role, lo, hi; hipStream_t s; };
     std::vector<Placed> placed;
@@ -859,31 +860,45 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     // the same emission bits; run se)
     p->pfrag = p->fuse && asr::dense_x3_on() && asr::rnn_x3_applies(c.B, c.H) && (c.B % 16) == 0 &&
                c.in <= 256 && (c.in % 4) == 0;
-    // HIP maps the process's streams round-robin onto GPU_MAX_HW_QUEUES
-    // hardware queues (default 4, read when the runtime starts), and streams
-    // that share a queue run one after another (C5, 5 streams on 4 queues:
-    // 1.03 M vs 3.48 M frames/s).  Fit the automatic schedule to the queues:
-    // no decode-CU share of the input projection first, then fewer
+    // HIP maps the process's UNMASKED streams round-robin onto
+    // GPU_MAX_HW_QUEUES hardware queues (default 4, read when the runtime
+    // starts), and streams that share a queue run one after another (C5, 5
+    // streams on 4 queues: 1.03 M vs 3.48 M frames/s).  A CU-masked stream
+    // (hipExtStreamCreateWithCUMask) gets a hardware queue of its own — the
+    // mask is a property of the queue — so only the unmasked streams count
+    // against the variable (measured round 6, run r6b, 20 / 5 steps, at
+    // GPU_MAX_HW_QUEUES=4 with the 24-queue schedule kept: C4 365.3 M, 256
+    // per GPU 224.6 M, C2 63.9 M frames/s, the same as at 24 queues, where
+    // round 5's fit of every stream to 4 queues gave 310.7 / 97.8 / 22.1 M).
+    // Fit the automatic schedule so that the unmasked streams fit the
+    // queues: no decode-CU share of the input projection first, then fewer
     // production streams and decodes in flight, the larger count first;
-    // explicit counts are kept as given.  asr_pipeline_get_streams reports
-    // the outcome.
+    // explicit counts are kept as given.  asr_pipeline_get_streams /
+    // asr_pipeline_get_queue_use report the outcome.
     {
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         p->hw_queues = (q && atoi(q) > 0) ? atoi(q) : 4;
         auto nstreams = [&] { return p->D + p->P + (p->grows > 0 ? 1 : 0) + (p->split ? 1 : 0); };
-        if (nstreams() > p->hw_queues && p->grows > 0) p->grows = 0;
+        // streams created without a CU mask (the layout below)
+        auto unmasked = [&] {
+            if (p->mode == SHARED) return p->dcus > 0 ? 0 : p->D + p->P + (p->grows > 0 ? 1 : 0);
+            const bool masked = p->gcu > 0 && !(p->mode == GROUPS2 && p->D == 1);
+            return (masked ? 0 : p->D + p->P) + (p->split ? 1 : 0);
+        };
+        if (unmasked() > p->hw_queues && p->grows > 0) p->grows = 0;
         // then production streams down to half the decodes in flight, then
         // both (small batches need both: C2 at 8 queues as D = 7, P = 1 ran
         // 16.4 M frames/s, at D = P = 4 38.7 M; at 16 queues D = 10, P = 6
         // 61.3 M against D = P = 8 53.9 M; runs sn, sn2)
-        while (nstreams() > p->hw_queues) {
+        while (unmasked() > p->hw_queues) {
             const bool canP = !c.prod_streams && p->P > 1, canD = !c.inflight && p->D > 1;
             if (canP && (!canD || p->P > (p->D + 1) / 2)) p->P--;
             else if (canD) p->D--;
             else break;
         }
-        p->tail_own = p->split && nstreams() < p->hw_queues;
+        p->tail_own = p->split && unmasked() < p->hw_queues;
         p->streams = nstreams() + (p->tail_own ? 1 : 0);
+        p->shared_queue_streams = unmasked() + (p->tail_own ? 1 : 0);
     }
     // drain hold (S > 1; A/B: ASR_PIPELINE_DRAIN=W held batches, -1: P - 1)
     // and the first segment's share of T (ASR_PIPELINE_SEG0, S = 2)
@@ -1116,6 +1131,13 @@ int asr_pipeline_get_groups(asr_pipeline_t* p, int* group) {
 int asr_pipeline_get_segments(asr_pipeline_t* p, int* segments) {
     if (!p || !segments) return ASR_ERR_ARG;
     *segments = p->S;
+    return ASR_OK;
+}
+
+int asr_pipeline_get_queue_use(asr_pipeline_t* p, int* shared_queue_streams, int* dedicated_queue_streams) {
+    if (!p) return ASR_ERR_ARG;
+    if (shared_queue_streams) *shared_queue_streams = p->shared_queue_streams;
+    if (dedicated_queue_streams) *dedicated_queue_streams = p->streams - p->shared_queue_streams;
     return ASR_OK;
 }
 

@@ -420,16 +420,20 @@ int asr_pipeline_describe(asr_pipeline_t* p, int* mode, int* inflight, int* prod
  * bit.  Any pointer may be NULL. */
 int asr_pipeline_get_production(asr_pipeline_t* p, int* fused, long long* decode_cu_rows, int* recurrence);
 /* Streams the pipeline created and the process's HIP hardware queues
- * (GPU_MAX_HW_QUEUES as read at create; HIP's default is 4).  HIP maps
- * streams round-robin onto the queues and streams that share a queue
- * serialise, so the automatic schedule is fitted to the queues (no
- * input-projection share on the decode CUs, then fewer production streams
- * down to half the decodes in flight, then both; the small-batch mode's
- * emission GEMMs get a stream of their own only when a queue is left for
- * it); streams > hw_queues only when the caller fixed inflight /
- * prod_streams.  A server should export GPU_MAX_HW_QUEUES=24 (>= 16) before
- * HIP starts: the measured cost of fewer queues is in INTEGRATION.md §3. */
+ * (GPU_MAX_HW_QUEUES as read at create; HIP's default is 4).  HIP maps the
+ * UNMASKED streams round-robin onto those queues (streams that share a queue
+ * serialise); a CU-masked stream gets a hardware queue of its own.  The
+ * pipeline's chip-filling and CU-group schedules mask their decode and
+ * production streams, so they need no GPU_MAX_HW_QUEUES setting (measured
+ * at HIP's default of 4: the same frames/s as at 24);
+ * only the unmasked ones (every stream with decode_cus = -1, the small-batch
+ * mode's GEMM streams) are fitted to the queues (no input-projection share
+ * on the decode CUs, then fewer production streams down to half the
+ * decodes in flight, then both), unless the caller fixed inflight /
+ * prod_streams.  asr_pipeline_get_queue_use: how many of the streams share
+ * HIP's queues and how many have a queue of their own. */
 int asr_pipeline_get_streams(asr_pipeline_t* p, int* streams, int* hw_queues);
+int asr_pipeline_get_queue_use(asr_pipeline_t* p, int* shared_queue_streams, int* dedicated_queue_streams);
 /* Where the pipeline's streams run: for each stream it created, its role
  * (ASR_PIPE_ROLE_*) and the CU range [cu_lo, cu_hi) of its CU mask
  * (hipExtStreamCreateWithCUMask bits; [0, ncu) = unmasked).  *n = streams

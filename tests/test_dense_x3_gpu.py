@@ -48,7 +48,10 @@ def _gemm(x, W, b, epi, arith_kind):
 
 @pytest.mark.parametrize("M,K,N,epi", [(1000, 256, 256, "bias"), (333, 96, 200, "none"), (64, 32, 64, "relu"),
                                        (4099, 128, 512, "bias"), (2000, 200, 300, "none"), (17, 4, 70, "bias"),
-                                       (140000, 256, 256, "none")])
+                                       (140000, 256, 256, "none"),
+                                       # K > 256: the large-K kernel (B split once, fragment-major, LDS-DMA)
+                                       (3000, 1024, 1024, "none"), (1000, 1024, 1000, "bias"), (257, 300, 70, "relu"),
+                                       (130, 2048, 129, "bias"), (4097, 512, 256, "none")])
 def test_gemm_fp32_accuracy(M, K, N, epi, arith):
     """Split-bf16 GEMM vs fp64: error / sum|a b| <= 1e-6 and no worse than the
     fp32 MFMA kernel's (x 1.5 + 1e-8); ragged M, K not a multiple of 32, N
@@ -94,6 +97,29 @@ def test_gemm_rows_independent_of_m(arith):
     # z = x . (W^T)^T through asr_matmul_tb: B read with strides, same products
     z = asr.DeviceMatrix(M, N)
     import ctypes
+    Wt = dm(np.ascontiguousarray(W.T))
+    xd = dm(x)
+    asr.check(asr.lib().asr_matmul_tb(xd.ptr, Wt.ptr, z.ptr, M, K, N, None), "asr_matmul_tb")
+    assert np.array_equal(z.toCpu(), full)
+
+
+def test_gemm_large_k_rows_independent_of_m(arith):
+    """K > 256 (the large-K split kernel): a sub-batch's rows are the whole
+    batch's bits (128-row tiles, XCD-ordered workgroups: the tile a row lands
+    in never changes its sums), and strided B (asr_matmul_tb) agrees."""
+    asr.set_dense_arith(asr.DENSE_SPLIT_BF16)
+    rng = np.random.default_rng(5)
+    M, K, N = 3000, 1024, 1000
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = (rng.uniform(-1, 1, (K, N)) / 32).astype(np.float32)
+    full = asr.DeviceMatrix(M, N)
+    asr.linear_fwd(dm(x), dm(W), None, full, asr.EPI_NONE)
+    full = full.toCpu()
+    for lo, hi in ((0, 16), (7, 1000), (2900, 3000)):
+        part = asr.DeviceMatrix(hi - lo, N)
+        asr.linear_fwd(dm(x[lo:hi]), dm(W), None, part, asr.EPI_NONE)
+        assert np.array_equal(part.toCpu(), full[lo:hi]), (lo, hi)
+    z = asr.DeviceMatrix(M, N)
     Wt = dm(np.ascontiguousarray(W.T))
     xd = dm(x)
     asr.check(asr.lib().asr_matmul_tb(xd.ptr, Wt.ptr, z.ptr, M, K, N, None), "asr_matmul_tb")
