@@ -280,41 +280,49 @@ C5P = GOLDEN / "c5_production.json"
 
 @pytest.mark.skipif(not C5P.exists(), reason="tests/golden/c5_production.json not generated")
 def test_c5_production_full_length_vs_oracle(monkeypatch):
-    """C5 at its full length on PRODUCTION emissions: the
-    bench's C5 model (H = 1024, V = 1000, 32 utterances, T = 2000) through the
-    library's fp32 dense arithmetic, log_softmax emissions — where the wide
-    kernel's orphan adoption fires (~0.1-0.2 per frame) — against the CPU
-    oracle's decode of the same bytes (tests/golden/c5_production.json,
-    written in the dev container by tests/golden/make_c5_production_golden.py
-    from tools/dump_c5_emissions.py's dump; the emission digests tie the
-    fixture to these bytes).  Four utterances x 2000 frames:
+    """C5 on PRODUCTION emissions: the bench's C5 model
+    (H = 1024, V = 1000, 32 utterances, T = 2000) through the library's fp32
+    dense arithmetic, log_softmax emissions — where every frame appends a
+    label and the wide kernel's orphan adoption fires — against the CPU
+    oracle's decode of the same bytes over their first g["T"] frames
+    (tests/golden/c5_production.json, written in the dev container by
+    tests/golden/make_c5_production_golden.py from tools/dump_c5_emissions.py's
+    dump; the emission digests tie the fixture to these bytes; the oracle's
+    string work grows ~T^1.75 on such emissions, ~3 h per utterance at T =
+    1000).  Four utterances:
       * the wide kernel, whole decode: best labels, beam size, ranked labels
         (digest) and every rank's log-prob within 1e-9 relative;
       * the same in two T-segments (the C5 pipeline's hand-off), bit for bit;
       * with every orphan adoption forced through the one-thread scan that
         runs past 128 filter hits per frame (ASR_CTC_WIDE_ADOPT_CAP=1), bit
         for bit;
-      * the four rows inside the whole 32-utterance batch, bit for bit."""
+      * the four rows inside the whole 32-utterance batch, bit for bit.
+    Then the full T = 2000 of the four utterances: whole = two T-segments
+    (property, bit for bit)."""
     sys.path.insert(0, str(ROOT / "tools"))
     import dump_c5_emissions as c5
     g = json.loads(C5P.read_text())
     e, em = c5.production_emissions(asr)
     T, B, V, beam = g["T"], g["B"], g["V"], g["beam"]
-    assert e.shape == (T, B, V)
+    Tp = g.get("T_production", T)
+    assert e.shape == (Tp, B, V)
     uids = g["utterances"]
     for u, d in zip(uids, g["emis_sha256"]):
         assert c5.digest(e[:, u, :]) == d, f"utterance {u}: emissions differ from the fixture's (regenerate it)"
-    sub = np.ascontiguousarray(e[:, uids, :])
+    sub = np.ascontiguousarray(e[:T, uids, :])
     d_sub = asr.DeviceMatrix.from_numpy(sub.reshape(T * len(uids), V))
 
-    def run(segments):
-        d = asr.CTCDecoder(V, beam, 0)
+    def run(segments, d_src=None, Tr=None, ns=None):
+        d_src = d_sub if d_src is None else d_src
+        Tr = T if Tr is None else Tr
         n = len(uids)
+        d = asr.CTCDecoder(V, beam, 0)
         if segments:
-            for t0, t1 in ((0, 1111), (1111, T)):
-                d.decode_segment(d_sub.ptr + 4 * t0 * n * V, T, t0, t1, n, True)
+            cut = Tr * 5 // 9
+            for t0, t1 in ((0, cut), (cut, Tr)):
+                d.decode_segment(d_src.ptr + 4 * t0 * n * V, Tr, t0, t1, n, True)
         else:
-            d.decode_device(d_sub.ptr, T, n, True)
+            d.decode_device(d_src.ptr, Tr, n, True)
         assert d.config()[1] == 8   # the wide kernel
         beams = d.beams(max_hyps=d.config()[0])
         d.close()
@@ -338,7 +346,15 @@ def test_c5_production_full_length_vs_oracle(monkeypatch):
     monkeypatch.setenv("ASR_CTC_WIDE_ADOPT_CAP", "1")
     same(run(False), "adoptions through the one-thread scan")
     monkeypatch.delenv("ASR_CTC_WIDE_ADOPT_CAP")
-    dec, best = decode_best(em.ptr, T, B, V, beam, True)
+    # the four rows inside the whole 32-utterance batch (its first T frames)
+    dec = asr.CTCDecoder(V, beam, 0)
+    dec.decode_device(em.ptr, T, B, True)
+    lab, lp = dec.best()
     dec.close()
     for i, u in enumerate(uids):
-        assert best[0][u] == whole[i][0][0] and best[1][u] == whole[i][0][1], f"utterance {u} in the batch"
+        assert lab[u] == whole[i][0][0] and lp[u] == whole[i][0][1], f"utterance {u} in the batch"
+    if Tp > T:   # C5's full T: whole = two T-segments, bit for bit
+        full = asr.DeviceMatrix.from_numpy(np.ascontiguousarray(e[:, uids, :]).reshape(Tp * len(uids), V))
+        a, b = run(False, full, Tp), run(True, full, Tp)
+        for i in range(len(uids)):
+            assert [l for l, _ in a[i]] == [l for l, _ in b[i]] and [x for _, x in a[i]] == [x for _, x in b[i]], uids[i]
