@@ -213,7 +213,7 @@ def load_profile_json(name: str):
 # profiles/<round>/ hold the counter summaries this line embeds: the newest
 # round that profiled the workload and kernel variant (every record names its
 # source run and commit)
-PROFILE_ROUNDS = ("r05", "r04", "r03")
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03")
 
 
 def decoder_variant(V: int, waves: int, max_states: int) -> str:

@@ -3,7 +3,7 @@
 set -e
 P=gpurun_out/${RUN:?}; R=${ROUND:-r05}
 mkdir -p profiles/$R
-SRC="gpurun_out/$RUN (rocprofv3 passes of bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-serialized: C4, two 1024-utterance pipeline batches per step, 4 decodes in flight, 2 T-segments; round-5 tree at commit $(git rev-parse --short HEAD))"
+SRC="gpurun_out/$RUN (rocprofv3 passes of bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-serialized: C4, two 1024-utterance pipeline batches per step, 4 decodes in flight, 2 T-segments; ${R} tree at commit $(git rev-parse --short HEAD))"
 python tools/traffic_from_pmc.py $P/fetch/run_counter_collection.csv $P/write/run_counter_collection.csv C4 "$SRC" $R | tail -3
 python tools/issue_from_pmc.py $P/sq/run_counter_collection.csv --kernel ctc_wave_kernel --T 500 --B 1024 --workload C4 --cus 128 --source "$SRC" --round $R | tail -5
 python tools/wait_from_pmc.py $P/wait/run_counter_collection.csv $P/issue/run_counter_collection.csv $P/sq/run_counter_collection.csv --T 500 --B 1024 --source "$SRC" --round $R | tail -5
