@@ -1145,9 +1145,8 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 // each other through memory inside the launch:
 //   * h_t is stored write-through (buffer stores with the sc1 bit) into hid
 //     (its final place); every storing wave drains its stores (vmcnt(0)),
-//     the workgroup barriers, and one lane records the frames it published
-//     (prog[wg]) and adds 1 to the launch's step counter (agent-scope
-//     atomic);
+//     the workgroup barriers, and one lane adds 1 to the launch's step
+//     counter (agent-scope atomic);
 //   * before frame t a workgroup's first lane polls the counter (agent-scope
 //     relaxed loads, s_sleep between) until all nWG workgroups have
 //     published frame t - 1, the workgroup barriers, and every load of
@@ -1166,8 +1165,9 @@ int rnn_step_mfma_multi_launch(float* const* hts, const float* const* hps, int n
 //     every workgroup that sees it (waiting, or dispatched late) exits;
 //   * a one-workgroup recovery kernel follows on the stream: it exits at
 //     once unless the abort word is set, and then computes every frame a
-//     tile had not published (prog[wg], which differs by at most one frame
-//     between workgroups) with the same arithmetic, so the call's bits are
+//     tile had not published (prog[wg], written as each workgroup leaves:
+//     the frame it stopped at; it differs by at most one frame between
+//     workgroups) with the same arithmetic, so the call's bits are
 //     those of an undisturbed launch (slower, never wrong);
 //   * each launch owns its control block (counter, abort word, prog[]) until
 //     an event recorded after its recovery kernel has completed.
@@ -1182,10 +1182,15 @@ constexpr unsigned long long RP_TIMEOUT = 50000000ull;   // 0.5 s of s_memrealti
 
 // One launch's control block (device memory; the head is zeroed on the
 // stream before the launch).
+// The counter, the abort word and the progress words sit on separate
+// 256-byte lines: with all three on one line (round 6's first layout) every
+// workgroup's progress store contended with the polled counter (C5's
+// recurrence 4.9 -> 6.4 us per frame).
 struct PersistCtl {
     unsigned ctr;              // publications: one per workgroup and frame
+    unsigned pad0[63];
     unsigned abort;            // 1: a workgroup gave up waiting
-    unsigned pad[14];
+    unsigned pad1[63];
     unsigned prog[RP_MAXWG];   // frames published, per workgroup
 };
 
@@ -1241,6 +1246,7 @@ struct RpTile {
     // h_t = tanhf((P_t + h_{t-1}.W_hh) + bias) of this thread's outputs (hp:
     // h_{t-1}; NULL: h_{-1} = 0, bias_tanh's formula), stored write-through.
     // rp_part: the workgroup's partial products (LDS); one barrier inside.
+    template <bool HOIST>
     __device__ __forceinline__ void frame(const float* hp, int sbytes, __amdgpu_buffer_rsrc_t rs_t,
                                           const float (&Pv)[EPT], f32x4* rp_part) const {
         const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1258,6 +1264,9 @@ struct RpTile {
                 for (int rb = 0; rb < RB; rb++)
                     a[i][rb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                              rs_p, (arow[rb] + 16 * i) * 4, 0, RP_SC1));
+            // every load of h_{t-1} in flight before the first MFMA (the
+            // scheduler otherwise keeps two in flight: KCH / 2 round trips)
+            if constexpr (HOIST) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < KCH; i++)
 #pragma unroll
@@ -1298,7 +1307,7 @@ struct RpTile {
 // stalls before that frame, as if it had lost its CU, until the others give
 // up (bounded: 2 s); then the launch ends aborted and the recovery kernel
 // finishes it.
-template <int RB, int NT, int KCH>
+template <int RB, int NT, int KCH, bool HOIST>
 __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const float* h0,
                                                                           const float* __restrict__ Whh,
                                                                           const float* __restrict__ b_ih,
@@ -1339,30 +1348,44 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_persist_kernel(const
                         __builtin_amdgcn_s_sleep(8);
                     rp_abort = 1;
                 }
-                while (!rp_abort && __hip_atomic_load(&ctl->ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                // the poll is one L2 round trip; the abort word and the clock
+                // are read every 16th poll only (a frame's wait is a few
+                // us, the abort's reaction stays far below the timeout):
+                // reading both on every poll doubled its period (C5's
+                // recurrence 5.9 -> 6.6 us per frame)
+                bool ab = rp_abort != 0;
+                unsigned spins = 0;
+                while (!ab && __hip_atomic_load(&ctl->ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                     __builtin_amdgcn_s_sleep(2);
+                    if ((++spins & 15u) != 0u) continue;
                     if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        rp_abort = 1;
+                        ab = true;
                     } else if (__builtin_amdgcn_s_memrealtime() - t0 > RP_TIMEOUT) {
-                        rp_abort = 1;
+                        ab = true;
                         __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store(host_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
+                if (ab) rp_abort = 1;
             }
             __syncthreads();
-            if (rp_abort) return;
+            if (rp_abort) {   // frames [0, t) published: the recovery starts this tile at t
+                if (tid == 0) __hip_atomic_store(&ctl->prog[wg], (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
         }
-        tile.frame(hp, sbytes, rs_t, Pv, rp_part);
-        // publish frame t: every wave's stores drained, then the workgroup's
-        // progress and one add to the counter
+        tile.template frame<HOIST>(hp, sbytes, rs_t, Pv, rp_part);
+        // publish frame t: every wave's stores drained, then one add to the
+        // counter
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
-            __hip_atomic_store(&ctl->prog[wg], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&ctl->ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (tid == 0) __hip_atomic_fetch_add(&ctl->ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the workgroup's progress is written once, when it leaves (T here, the
+    // frame it stopped at on an abort, 0 from the memset if it never ran): a
+    // store per frame, which the next frame's first wait drains, cost C5's
+    // recurrence ~0.5 us per frame
+    if (tid == 0) __hip_atomic_store(&ctl->prog[wg], (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // After every one-launch recurrence, on its stream: nothing unless the launch
@@ -1395,7 +1418,7 @@ __global__ __launch_bounds__(64 * RSM_WAVES) void rnn_recur_recover_kernel(const
             tile.setup(Whh, b_ih, b_hh, q % gx, q / gx, B, H);
             float Pv[EPT];
             tile.load_p(rs_t, Pv);
-            tile.frame(hp, sbytes, rs_t, Pv, rp_part);
+            tile.template frame<false>(hp, sbytes, rs_t, Pv, rp_part);
             __syncthreads();   // rp_part is the next tile's
         }
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1417,6 +1440,7 @@ struct PersistSlot {
     bool used = false;
     int nwg = 0;               // workgroups of its launch
     bool plain = false;        // a launch without a pipeline CU hint
+    hipStream_t stream = nullptr;
 };
 struct PersistPool {
     std::mutex mu;
@@ -1443,20 +1467,24 @@ bool persist_reap(PersistPool& pp, PersistSlot& s) {
 template <int RB, int NT, int KCH>
 static int launch_persist(const float* h0, const float* Whh, const float* b_ih, const float* b_hh, float* hid,
                           int T, int B, int H, PersistSlot& slot, int fault_frame, hipStream_t s) {
+    // every load of h_{t-1} in flight at once from H = 1024 (KCH = 8) on:
+    // alone (tools/step_time.py, run r6m4) 32 x 1024 5.12 -> 4.71 us per
+    // frame, 64 x 1024 6.07 -> 5.44; at H = 512 (KCH = 4) slower, 3.36 -> 3.63
+    constexpr bool HOIST = KCH >= 8;
     static AsrAttrOnce attr, attr_r;
-    if (int r_ = attr.set((const void*)rnn_recur_persist_kernel<RB, NT, KCH>, RP_LDS)) return r_;
+    if (int r_ = attr.set((const void*)rnn_recur_persist_kernel<RB, NT, KCH, HOIST>, RP_LDS)) return r_;
     if (int r_ = attr_r.set((const void*)rnn_recur_recover_kernel<RB, NT, KCH>, RP_LDS)) return r_;
     static std::once_flag occ_once;
     static int occ = 0;
     std::call_once(occ_once, [] {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, rnn_recur_persist_kernel<RB, NT, KCH>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, rnn_recur_persist_kernel<RB, NT, KCH, HOIST>,
                                                          64 * RSM_WAVES, RP_LDS) != hipSuccess)
             occ = 0;
     });
     if (occ < 1) return ASR_ERR_UNSUPPORTED;   // one workgroup must fit a CU
     const int gx = H / (16 * NT), gy = (B + 16 * RB - 1) / (16 * RB);
     ASR_HIP_TRY(hipMemsetAsync(slot.ctl, 0, offsetof(PersistCtl, prog) + sizeof(unsigned) * gx * gy, s));
-    hipLaunchKernelGGL((rnn_recur_persist_kernel<RB, NT, KCH>), dim3((unsigned)gx, (unsigned)gy),
+    hipLaunchKernelGGL((rnn_recur_persist_kernel<RB, NT, KCH, HOIST>), dim3((unsigned)gx, (unsigned)gy),
                        dim3(64 * RSM_WAVES), RP_LDS, s, h0, Whh, b_ih, b_hh, hid, T, B, H, slot.ctl, slot.status_d,
                        fault_frame);
     ASR_LAUNCH_TRY();
@@ -1487,11 +1515,15 @@ int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_i
     std::lock_guard<std::mutex> lock(pp.mu);
     auto& slots = pp.slots[dev];
     PersistSlot* slot = nullptr;
-    int reserved = 0;   // workgroups of plain launches still in flight on this device
+    // workgroups of plain launches still in flight on this device's OTHER
+    // streams (a launch queued behind another on its own stream never shares
+    // the CUs with it: counting those sent back-to-back calls on one stream
+    // to the per-frame steps)
+    int reserved = 0;
     for (auto& q : slots) {
         if (persist_reap(pp, q)) {
             if (!slot) slot = &q;
-        } else if (q.plain) {
+        } else if (q.plain && q.stream != s) {
             reserved += q.nwg;
         }
     }
@@ -1542,6 +1574,7 @@ int rnn_recur_persist_launch(const float* h0, const float* Whh, const float* b_i
     slot->used = true;
     slot->nwg = nwg;
     slot->plain = plain;
+    slot->stream = s;
     pp.launches++;
     return ASR_OK;
 }
