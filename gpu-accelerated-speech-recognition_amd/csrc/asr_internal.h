@@ -74,6 +74,16 @@ extern thread_local int asr_internal_dense_arith;
 // apply (V > 63, .cu semantics, timesteps).  For the pipeline's schedule.
 struct asr_ctc;
 int asr_internal_ctc_wave_occupancy(asr_ctc* h);
+// The wide decoder's first-tile precompute (ctc_tile0_kernel) queued by the
+// caller instead of ahead of each decode launch: _external(h, B, T) sizes the
+// handle's workspace for B x T and switches the decode's own precompute off
+// (ASR_ERR_UNSUPPORTED when the handle takes none: V <= 65); _tile0 fills
+// frames [t0, t1) of the B utterances from d_emis (at frame t0) on stream s.
+// The records are the decode's own (same kernel), so the bits do not change;
+// the caller orders them before the decode of those frames.
+int asr_internal_ctc_tile0_external(asr_ctc* h, int B, int T);
+int asr_internal_ctc_tile0(asr_ctc* h, const float* d_emis, int T, int t0, int t1, int B, long frame_stride,
+                           long utt_stride, hipStream_t s);
 // The recurrence (h0 = 0) of nb <= 4 equal-shape batches at once, in place
 // over each hids[j] [T*B, H] (holding x.W_ih on entry): H > 256 runs one
 // per-frame MFMA step launch for all of them (the step is latency-bound, so

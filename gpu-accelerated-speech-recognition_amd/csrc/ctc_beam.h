@@ -46,6 +46,7 @@ struct CtcArgs {
     double* best_score;     // [B]
     uint64_t* stamps;       // [B][NSTAMP] phase clocks (diagnostic build only)
     uint32_t* tile0;        // [B][T][WREC] first label tile per frame (wide kernel, V > 65; NULL: in-kernel)
+    int tile0_ext;          // 1: the caller filled tile0 for this launch's frames (ctc_launch_tile0 on its stream)
     int diag;               // bit 0: the wide kernel always takes its register fallback (tests; ASR_CTC_WIDE_FALLBACK=1);
                             // bit 1: its adoption list holds no hit: every adoption takes the one-thread scan (tests; ASR_CTC_WIDE_ADOPT_CAP=1)
     // Segmented decode (asr_ctc_decode_segment; one-wave kernel only): this
@@ -75,6 +76,7 @@ int ctc_occupancy(const CtcGeom& g, int waves);
 constexpr int WIDE_VMAX = 4096;   // largest vocabulary of the wide kernel (ctc_wide_kernel.inc)
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s);
 size_t ctc_tile0_bytes(int B, int T);   // a.tile0 workspace of the wide kernel
+int ctc_launch_tile0(const CtcArgs& a, hipStream_t s);   // a.tile0 for frames [a.t0, a.t1) (a.emis at a.t0)
 size_t ctc_lds_bytes_wide(int kc, int V);
 size_t ctc_seg_bytes_wide(int kc);   // saved beam per utterance between segments (wide kernel)
 int ctc_set_max_lds_wide();

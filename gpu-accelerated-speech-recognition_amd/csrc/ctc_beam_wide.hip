@@ -7,13 +7,18 @@ namespace asr {
 
 size_t ctc_tile0_bytes(int B, int T) { return sizeof(uint32_t) * WREC * (size_t)B * T; }
 
+int ctc_launch_tile0(const CtcArgs& a, hipStream_t s) {
+    if (!a.tile0 || a.g.V - 1 <= WTILE || a.g.V > WVMAX || a.t1 <= a.t0) return ASR_ERR_ARG;
+    // the launch's frames [t0, t1) (a segment of a segmented decode)
+    hipLaunchKernelGGL(ctc_tile0_kernel, dim3((unsigned)(a.B * (a.t1 - a.t0))), dim3(64), sizeof(uint32_t) * a.g.V,
+                       s, a, a.tile0);
+    ASR_LAUNCH_TRY();
+    return ASR_OK;
+}
+
 int ctc_launch_decode_wide(const CtcArgs& a, int rpt, hipStream_t s) {
-    if (a.tile0) {   // every frame's first tile (ctc_tile0_kernel), then the decode
-        if (a.g.V - 1 <= WTILE || a.g.V > WVMAX) return ASR_ERR_ARG;
-        // the launch's frames [t0, t1) (a segment of a segmented decode)
-        hipLaunchKernelGGL(ctc_tile0_kernel, dim3((unsigned)(a.B * (a.t1 - a.t0))), dim3(64), sizeof(uint32_t) * a.g.V,
-                           s, a, a.tile0);
-        ASR_LAUNCH_TRY();
+    if (a.tile0 && !a.tile0_ext) {   // every frame's first tile (ctc_tile0_kernel), then the decode
+        if (int rc = ctc_launch_tile0(a, s)) return rc;
     }
     const size_t lds = ctc_lds_bytes(a.g);
     const dim3 grid(a.B), block(WNT);

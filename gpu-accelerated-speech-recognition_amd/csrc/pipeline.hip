@@ -79,6 +79,7 @@ struct asr_pipeline {
     int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
     double seg0 = 0.0;    // first segment's share of T when S = 2 (0: T / 2)
+    bool tile0_prod = false;   // the wide decoder's first tiles computed by the production (produce_full_segments)
     // Drain (S > 1): the last decode segment of the newest `hold` batches is
     // held back.  A newer batch releases the oldest onto its decode stream
     // (the steady state); when the caller drains (collects a batch within D
@@ -238,6 +239,10 @@ int produce_full_segments(asr_pipeline* p, long i, const float* x, hipStream_t s
         asr_internal_rnn_kind = -1;
         if (!rc) rc = asr_linear_fwd(hs, p->W_out, p->b_out, p->emis[k] + r0 * c.V, (int)rows, c.H, c.V,
                                      ASR_EPI_BIAS_LOGSOFTMAX, sp);
+        // the wide decoder's first-tile records of these frames, here on the
+        // production CUs instead of ahead of the decode on its CU group
+        if (!rc && p->tile0_prod)
+            rc = asr_internal_ctc_tile0(p->dec[k], p->emis[k] + r0 * c.V, c.T, t0, t1, c.B, (long)c.B * c.V, c.V, sp);
         if (rc) return rc;
         ASR_HIP_TRY(hipEventRecord(p->ev_seg[(size_t)k * p->S + s], sp));
     }
@@ -981,6 +986,18 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
         if (!rc && conc > 1) rc = asr_ctc_set_concurrency(h, conc);
         // chip-filling batches: many utterances per decode CU, the one-wave kernel
         if (!rc && p->mode == SHARED && occw > 0) rc = asr_ctc_set_waves(h, ASR_CTC_WAVES_LIST);
+        // segmented unfused production with the wide decoder (C5): the
+        // first-tile precompute runs on the production stream (A/B:
+        // ASR_PIPELINE_TILE0_PROD=0 leaves it ahead of each decode launch)
+        if (!rc && k == 0 && p->S > 1 && !p->fuse && c.V + 1 > 64) {
+            const char* te = getenv("ASR_PIPELINE_TILE0_PROD");
+            p->tile0_prod = !(te && te[0] == '0');
+        }
+        if (!rc && p->tile0_prod) {
+            const int r = asr_internal_ctc_tile0_external(h, c.B, c.T);
+            if (r == ASR_ERR_UNSUPPORTED && k == 0) p->tile0_prod = false;   // no precompute for this V
+            else if (r) rc = r;
+        }
         for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec}) {
             hipEvent_t e = nullptr;
             if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = ASR_ERR_HIP;

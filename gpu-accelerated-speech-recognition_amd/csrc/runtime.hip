@@ -495,6 +495,7 @@ struct asr_ctc {
     uint64_t* d_fin_ts = nullptr;    // [B][kcap][2] append frames of the final tails
     uint32_t* d_tile0 = nullptr;     // [B][T] first label tile per frame (wide kernel, V > 65)
     bool tile0 = true;               // precompute first tiles (ASR_CTC_TILE0=0: in-kernel, for A/B timing)
+    bool tile0_ext = false;          // the caller queues the precompute (asr_internal_ctc_tile0)
     int diag = 0;                    // CtcArgs::diag (ASR_CTC_WIDE_FALLBACK=1: bit 0, ASR_CTC_WIDE_ADOPT_CAP=1: bit 1)
     size_t cap_all = 0;
     // pinned host mirrors of the best-path results
@@ -700,6 +701,31 @@ int asr_internal_rnn_recur_multi(const float* W_hh, const float* b_ih, const flo
 int asr_internal_ctc_wave_occupancy(asr_ctc* h) {
     if (!h || h->cu_mode || h->ts || !asr::ctc_wave_supported(plan(h, -1), 0)) return 0;
     return asr::ctc_occupancy_wave(plan(h, -1));
+}
+
+int asr_internal_ctc_tile0_external(asr_ctc* h, int B, int T) {
+    if (!h || B < 1 || T < 1) return ASR_ERR_ARG;
+    if (!use_tile0(h)) return ASR_ERR_UNSUPPORTED;
+    if (int rc = ensure_ws(h, B, T)) return rc;
+    h->tile0_ext = true;
+    return ASR_OK;
+}
+
+int asr_internal_ctc_tile0(asr_ctc* h, const float* d_emis, int T, int t0, int t1, int B, long frame_stride,
+                           long utt_stride, hipStream_t s) {
+    if (!h || !d_emis || !h->tile0_ext || t0 < 0 || t1 <= t0 || t1 > T || B < 1) return ASR_ERR_ARG;
+    if (B > h->capB || T > h->capT || !h->d_tile0) return ASR_ERR_STATE;   // sized by _external
+    asr::CtcArgs a{};
+    a.g = plan(h, 8);   // the wide kernel's geometry (V, blank)
+    a.emis = d_emis;
+    a.tstride = frame_stride;
+    a.ustride = utt_stride;
+    a.T = T;
+    a.B = B;
+    a.t0 = t0;
+    a.t1 = t1;
+    a.tile0 = h->d_tile0;
+    return asr::ctc_launch_tile0(a, s);
 }
 
 extern "C" {
@@ -928,6 +954,7 @@ int decode_frames(asr_ctc* h, const float* d_emis, int T, int B, long frame_stri
     a.nodes_ts = h->ts ? h->d_nodes_ts : nullptr;
     a.fin_ts = h->ts ? h->d_fin_ts : nullptr;
     a.tile0 = use_tile0(h) ? h->d_tile0 : nullptr;
+    a.tile0_ext = a.tile0 && h->tile0_ext ? 1 : 0;
     a.diag = h->diag;
     a.t0 = 0;
     a.t1 = segmented ? t1 : T;
