@@ -158,3 +158,27 @@ def test_oracle_timesteps_properties():
     # T = 1: every hypothesis is one label appended at frame 0
     one = oracle.decode_ts(emis[:1], beam, 0)
     assert all(fr == [0] * len(lab) for u in one for lab, _, fr in u)
+
+
+def test_c5_production_fixture_consistent():
+    """tests/golden/c5_production.json (the oracle's decode of the first T
+    frames of four C5 production-emission utterances, checked against the
+    wide kernel by test_full_configs_gpu.py) is self-consistent: a full beam
+    (beam + ties) per utterance, ranked by log-probability, the best
+    hypothesis first, labels inside the vocabulary with no blank, at most one
+    label per frame."""
+    p = GOLDEN / "c5_production.json"
+    if not p.exists():
+        pytest.skip("fixture not generated")
+    g = json.loads(p.read_text())
+    assert g["T"] <= g["T_production"] and g["V"] == 1000 and g["beam"] == 200
+    n = len(g["utterances"])
+    assert len(g["emis_sha256"]) == len(g["best_labels"]) == len(g["beam_logp"]) == len(g["n_hyps"]) == n
+    for i in range(n):
+        lp = g["beam_logp"][i]
+        assert len(lp) == g["n_hyps"][i] >= g["beam"]
+        assert all(a >= b for a, b in zip(lp, lp[1:]))
+        assert lp[0] == g["best_logp"][i] and math.isfinite(lp[0])
+        lab = g["best_labels"][i]
+        assert 0 < len(lab) <= g["T"]
+        assert all(0 < c < g["V"] for c in lab)   # blank 0 never emitted
