@@ -593,6 +593,10 @@ def main():
     ap.add_argument("--pipeline-batch", type=int, default=0,
                     help="utterances per pipeline batch (the rank's B go through as B / N batches; "
                          "0 = auto: 1024 when B is a larger multiple of it on the split-bf16 arithmetic)")
+    ap.add_argument("--coalesce", type=int, default=0,
+                    help="dynamic batching in the native pipeline (asr_pipeline_create_coalesced): this many "
+                         "consecutive submits run as one batch (1 = off; 0 = auto: submits of fewer than 128 "
+                         "utterances in launches of ~640 (C2: 10), else 1)")
     ap.add_argument("--py-pipeline", action="store_true",
                     help="the round-2 Python orchestration over torch streams instead of the library's "
                          "native pipeline (asr_pipeline_*); implied by its Python-only knobs")
@@ -1188,9 +1192,15 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
         del xh
     else:
         xs = [d_x]
+    # dynamic batching: C2's 64-utterance steps as launches of 640 (run r6cc,
+    # 20 / 5: 1 / 4 / 10 / 20 submits per launch 66.0 / 104.7 / 113.0 / 82.6 M
+    # frames/s; 256 per GPU 1 / 2 / 4: 221.1 / 232.4 / 213.8 M, 512 per GPU 1 / 2:
+    # 303.5 / 266.6 M — larger batches already fill the chip, and fewer,
+    # larger batches lengthen the fill and the drain)
+    cg = args.coalesce if args.coalesce > 0 else (min(10, max(1, 640 // Bp)) if Bp < 128 else 1)
     pl = asr.Pipeline(T, Bp, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
                       inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus,
-                      segments=args.segments)
+                      segments=args.segments, coalesce=cg)
     desc = pl.describe()
     if desc["mode"] == asr.PIPELINE_MODES[1] and H <= 256:
         # the pipeline's MFMA recurrence for chip-filling batches, also for
@@ -1198,7 +1208,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
         asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
     # results of batch i are read once the pipeline's buffers hold newer work:
     # D decoding and P producing
-    lag = desc["inflight"] + desc["prod_streams"]
+    lag = (desc["inflight"] + desc["prod_streams"]) * cg   # submits: cg per pipeline batch
     kernel_ms = []
     best = {}
 
@@ -1232,7 +1242,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     take.j = 0
     take.wait = 0.0
 
-    run(-(-(2 * (desc["inflight"] + desc["prod_streams"]) + 1) // nsub))   # every buffer, stream and workspace once
+    run(-(-(2 * (desc["inflight"] + desc["prod_streams"]) + 1) * cg // nsub))   # every buffer, stream and workspace once
     # priming: the GPU's clocks settle under this load before the W warmup
     # steps (untimed, like the line above; --prime-s 0 skips it)
     tp = time.perf_counter()
@@ -1262,7 +1272,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     stages = None
     if timeline:
         _, stamps = pl.timeline()
-        stages = stage_figures(stamps, 1e3 * elapsed, 1e3 * take.wait, args.steps, nsub, desc["inflight"])
+        stages = stage_figures(stamps, 1e3 * elapsed, 1e3 * take.wait, args.steps, nsub / cg, desc["inflight"])
         if os.environ.get("ASR_BENCH_TIMELINE"):   # diagnostics: the raw per-batch stamps
             np.savetxt(os.environ["ASR_BENCH_TIMELINE"], stamps, fmt="%.4f",
                        header="production start, production end, decode start, decode end (ms)")
@@ -1327,7 +1337,7 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
                       f"region)"}
     finish(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong, elapsed, kernel_ms,
            (lab, ln, lp), (kcap, desc["decode_waves"], 0), weights, hid0, em0, em_last,
-           {"pipeline_batch": Bp, "batches_per_step": nsub,
+           {"pipeline_batch": Bp, "batches_per_step": nsub, "coalesce": cg,
             "inflight_decodes": desc["inflight"], "production_streams": desc["prod_streams"],
             "decode_cus": desc["decode_cus"], "fused_emission": fused,
             "recurrence": desc["recurrence"], "streams": desc["streams"], "hw_queues": desc["hw_queues"],

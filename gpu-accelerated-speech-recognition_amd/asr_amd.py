@@ -61,7 +61,7 @@ EXPORTS = [
     "asr_pipeline_describe", "asr_pipeline_get_production", "asr_pipeline_get_streams", "asr_pipeline_get_queue_use",
     "asr_pipeline_peek_emissions", "asr_pipeline_get_segments", "asr_pipeline_get_drain", "asr_pipeline_get_groups",
     "asr_pipeline_get_placement", "asr_pipeline_probe_placement", "asr_pipeline_set_timing",
-    "asr_pipeline_get_timeline", "asr_pipeline_destroy",
+    "asr_pipeline_get_timeline", "asr_pipeline_destroy", "asr_pipeline_create_coalesced", "asr_pipeline_get_coalesce",
 ]
 # asr_pipeline_get_placement roles (ASR_PIPE_ROLE_*)
 PIPE_ROLES = {0: "decode", 1: "production", 2: "decode_cu_gemm", 3: "gemm"}
@@ -124,6 +124,8 @@ def lib() -> ctypes.CDLL:
         "asr_get_dense_arith": [ctypes.POINTER(_i)],
         "asr_rnn_emit_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
         "asr_pipeline_create": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)],
+        "asr_pipeline_create_coalesced": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)],
+        "asr_pipeline_get_coalesce": [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)],
         "asr_pipeline_submit": [_vp, _vp],
         "asr_pipeline_collect": [_vp, _vp, _i, _vp, _vp, _vp],
         "asr_pipeline_pending": [_vp, ctypes.POINTER(_i)],
@@ -618,13 +620,23 @@ class Pipeline:
     (labels [B][T], lengths [B], logp [B], decode_ms)."""
 
     def __init__(self, T: int, B: int, inp: int, H: int, V: int, beam: int, weights, blank: int = 0,
-                 inflight: int = 0, prod_streams: int = 0, decode_cus: int = 0, segments: int = 0):
+                 inflight: int = 0, prod_streams: int = 0, decode_cus: int = 0, segments: int = 0,
+                 coalesce: int = 1):
+        """coalesce > 1: dynamic batching (asr_pipeline_create_coalesced):
+        `coalesce` consecutive submits of B utterances run as one batch; the
+        schedule (inflight, prod_streams, ...) is that batch's."""
         self.T, self.B = T, B
+        self.coalesce = max(1, int(coalesce))
         self.cfg = PipelineConfig(T, B, inp, H, V, beam, blank, inflight, prod_streams, decode_cus, segments)
         self._w = weights   # (W_ih, W_hh, b_ih, b_hh, W_out, b_out) DeviceMatrix: kept alive
         h = _vp()
-        check(lib().asr_pipeline_create(ctypes.byref(self.cfg), *[w.ptr for w in weights], ctypes.byref(h)),
-              "asr_pipeline_create")
+        if self.coalesce > 1:
+            check(lib().asr_pipeline_create_coalesced(ctypes.byref(self.cfg), self.coalesce,
+                                                      *[w.ptr for w in weights], ctypes.byref(h)),
+                  "asr_pipeline_create_coalesced")
+        else:
+            check(lib().asr_pipeline_create(ctypes.byref(self.cfg), *[w.ptr for w in weights], ctypes.byref(h)),
+                  "asr_pipeline_create")
         self.h = h.value
         self._lab = np.zeros((B, max(T, 1)), np.int32)
         self._len = np.zeros(B, np.int32)
@@ -653,7 +665,8 @@ class Pipeline:
                 "decode_cu_gemm_rows": gr.value, "recurrence": rk.value, "streams": ns.value,
                 "hw_queues": hq.value, "segments": sg.value, "groups": gp.value,
                 "drain_held_batches": hb.value, "first_segment_share": round(f0.value, 4),
-                "shared_queue_streams": qs.value, "dedicated_queue_streams": qd.value}
+                "shared_queue_streams": qs.value, "dedicated_queue_streams": qd.value,
+                "coalesce": self.coalesce}
 
     def placement(self):
         """[(role name, cu_lo, cu_hi)] of every stream the pipeline created."""
@@ -729,8 +742,13 @@ class Pipeline:
         decode consumed (asr_pipeline_peek_emissions)."""
         ptr = _vp()
         check(lib().asr_pipeline_peek_emissions(self.h, ctypes.byref(ptr)), "asr_pipeline_peek_emissions")
-        out = np.empty((self.T, self.B, self.cfg.V), np.float32)
+        g, col = self.coalesce, _i()
+        if g > 1:   # the whole coalesced batch, then this submit's columns
+            check(lib().asr_pipeline_get_coalesce(self.h, None, None, ctypes.byref(col)), "asr_pipeline_get_coalesce")
+        out = np.empty((self.T, g * self.B, self.cfg.V), np.float32)
         check(lib().asr_memcpy_d2h(_ptr(out), ptr.value, out.nbytes, None), "asr_memcpy_d2h")
+        if g > 1:
+            out = np.ascontiguousarray(out[:, col.value * self.B:(col.value + 1) * self.B, :])
         return out
 
     def close(self) -> None:

@@ -79,6 +79,16 @@ struct asr_pipeline {
     int gtiled = 0;       // ... with the tiled GEMM kernel, row tiles per workgroup (0: persistent)
     int S = 1;            // T-segments per batch (fused production only)
     double seg0 = 0.0;    // first segment's share of T when S = 2 (0: T / 2)
+    // Dynamic batching (asr_pipeline_create_coalesced): cg consecutive
+    // submits of Bo utterances each are one pipeline batch of cfg.B = cg * Bo
+    // utterances (one production and one decode launch for all of them).
+    int cg = 1, Bo = 0;
+    std::vector<float*> stage;   // inputs [T][cfg.B][in] of the batches being assembled / in flight
+    int cfill = 0;               // columns of pipeline batch `submitted` filled so far
+    std::deque<std::pair<long, int>> opend;   // caller's uncollected batches: (pipeline batch, column)
+    Result ocache;               // the pipeline batch whose rows collects are returning
+    long ocache_q = -1;
+    int ocol = 0;                // column of the caller's batch collected last
     bool tile0_prod = false;   // the wide decoder's first tiles computed by the production (produce_full_segments)
     // Drain (S > 1): the last decode segment of the newest `hold` batches is
     // held back.  A newer batch releases the oldest onto its decode stream
@@ -593,6 +603,7 @@ void release(asr_pipeline* p) {
     for (auto b : p->hid) hipFree(b);
     for (auto b : p->emis) hipFree(b);
     for (auto b : p->hst) hipFree(b);
+    for (auto b : p->stage) hipFree(b);
     for (auto e : p->ev_seg) if (e) hipEventDestroy(e);
     for (auto e : p->ev_dpre) if (e) hipEventDestroy(e);
     for (auto* v : {&p->ev_ready, &p->ev_free, &p->ev_proj, &p->ev_rec, &p->ev_t[0], &p->ev_t[1], &p->ev_t[2],
@@ -1013,9 +1024,11 @@ int asr_pipeline_create(const asr_pipeline_config* cfg, const float* W_ih, const
     return ASR_OK;
 }
 
-int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
-    if (!p || !x) return ASR_ERR_ARG;
-    ArithGuard arith_guard(p->arith);
+}  // extern "C"
+
+namespace {
+
+int submit_batch(asr_pipeline* p, const float* x) {
     if (p->fail_rc) return p->fail_rc;
     const long i = p->submitted;
     // buffer i % nbuf is reused: its previous batch's results must be fetched first
@@ -1070,10 +1083,101 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
     return rc;
 }
 
+// Dynamic batching: the caller's batch goes into columns [j Bo, (j + 1) Bo)
+// of the pipeline batch being assembled (a strided copy on the production
+// stream that batch will run on); the cg-th submit queues the pipeline batch.
+int submit_coalesced(asr_pipeline* p, const float* x) {
+    if (p->fail_rc) return p->fail_rc;
+    const auto& c = p->cfg;
+    const long q = p->submitted;   // the pipeline batch being assembled
+    const long ns = (long)p->stage.size();
+    if (p->cfill == 0)   // stage q % ns was read by pipeline batch q - ns: fetched (stashed) first
+        while (q - ns >= p->collected) {
+            Result r;
+            if (int rc = fetch(p, r)) return rc;
+            p->stash.push_back(std::move(r));
+        }
+    const int j = p->cfill;
+    const size_t row = sizeof(float) * (size_t)p->Bo * c.in;
+    ASR_HIP_TRY(hipMemcpy2DAsync(p->stage[q % ns] + (size_t)j * p->Bo * c.in, sizeof(float) * (size_t)c.B * c.in, x,
+                                 row, row, c.T, hipMemcpyDeviceToDevice, p->s_prod[q % p->P]));
+    p->opend.emplace_back(q, j);
+    if (++p->cfill < p->cg) return ASR_OK;
+    p->cfill = 0;
+    const int rc = submit_batch(p, p->stage[q % ns]);
+    if (rc && p->submitted == q) {   // not accepted: this submit may come again
+        p->opend.pop_back();
+        p->cfill = p->cg - 1;
+    }
+    return rc;
+}
+
+// The results of pipeline batch q: a partial batch (the caller collects
+// before cg submits) is completed with zero features, whose rows are decoded
+// and dropped.
+int coalesced_result(asr_pipeline* p, long q) {
+    if (p->ocache_q == q) return ASR_OK;
+    const auto& c = p->cfg;
+    if (q >= p->submitted) {
+        float* st = p->stage[q % (long)p->stage.size()];
+        const int have = p->cfill;
+        ASR_HIP_TRY(hipMemset2DAsync(st + (size_t)have * p->Bo * c.in, sizeof(float) * (size_t)c.B * c.in, 0,
+                                     sizeof(float) * (size_t)(p->cg - have) * p->Bo * c.in, c.T, p->s_prod[q % p->P]));
+        p->cfill = 0;
+        if (int rc = submit_batch(p, st)) return rc;
+    }
+    Result r;
+    if (!p->stash.empty()) {
+        r = std::move(p->stash.front());
+        p->stash.pop_front();
+    } else if (int rc = fetch(p, r)) {
+        return rc;
+    }
+    p->ocache = std::move(r);
+    p->ocache_q = q;
+    return ASR_OK;
+}
+
+int collect_coalesced(asr_pipeline* p, int32_t* labels, int max_len, int32_t* lengths, double* logp,
+                      float* decode_ms) {
+    if (p->opend.empty()) return ASR_ERR_STATE;
+    const long q = p->opend.front().first;
+    const int col = p->opend.front().second;
+    if (int rc = coalesced_result(p, q)) return rc;
+    const auto& c = p->cfg;
+    const Result& r = p->ocache;
+    const int b0 = col * p->Bo;
+    for (int b = 0; b < p->Bo; b++) {
+        const int len = r.len[b0 + b];
+        if (lengths) lengths[b] = len;
+        if (logp) logp[b] = r.lp[b0 + b];
+        if (labels) {
+            const int n = std::min(len, max_len);
+            std::memcpy(labels + (size_t)b * max_len, r.lab.data() + (size_t)(b0 + b) * c.T, sizeof(int32_t) * n);
+        }
+    }
+    if (decode_ms) *decode_ms = r.ms;
+    p->returned = r.batch;
+    p->ocol = col;
+    p->opend.pop_front();
+    return r.rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int asr_pipeline_submit(asr_pipeline_t* p, const float* x) {
+    if (!p || !x) return ASR_ERR_ARG;
+    ArithGuard arith_guard(p->arith);
+    return p->cg > 1 ? submit_coalesced(p, x) : submit_batch(p, x);
+}
+
 int asr_pipeline_collect(asr_pipeline_t* p, int32_t* labels, int max_len, int32_t* lengths, double* logp,
                          float* decode_ms) {
     if (!p || (!labels && max_len > 0)) return ASR_ERR_ARG;
     ArithGuard arith_guard(p->arith);   // a drain may queue held-back production
+    if (p->cg > 1) return collect_coalesced(p, labels, max_len, lengths, logp, decode_ms);
     if (p->stash.empty()) {   // the common case: straight into the caller's arrays
         long batch = -1;
         int res = ASR_OK;
@@ -1108,9 +1212,47 @@ int asr_pipeline_peek_emissions(asr_pipeline_t* p, const float** d_emis) {
     return ASR_OK;
 }
 
+int asr_pipeline_create_coalesced(const asr_pipeline_config* cfg, int group, const float* W_ih, const float* W_hh,
+                                  const float* b_ih, const float* b_hh, const float* W_out, const float* b_out,
+                                  asr_pipeline_t** out) {
+    if (!cfg || !out || group < 1 || cfg->B < 1 || (long)cfg->B * group > (1L << 20)) return ASR_ERR_ARG;
+    if (group == 1) return asr_pipeline_create(cfg, W_ih, W_hh, b_ih, b_hh, W_out, b_out, out);
+    asr_pipeline_config c = *cfg;
+    c.B = cfg->B * group;
+    if (int rc = asr_pipeline_create(&c, W_ih, W_hh, b_ih, b_hh, W_out, b_out, out)) return rc;
+    asr_pipeline* p = *out;
+    // the caller's features are copied onto the production stream that reads
+    // them: schedules whose input projection runs elsewhere are not coalesced
+    if (p->split || p->G > 1 || p->grows > 0) {
+        asr_pipeline_destroy(p);
+        *out = nullptr;
+        return ASR_ERR_UNSUPPORTED;
+    }
+    p->cg = group;
+    p->Bo = cfg->B;
+    for (int k = 0; k <= p->nbuf; k++) {
+        float* b = nullptr;
+        if (hipMalloc(&b, sizeof(float) * (size_t)c.T * c.B * c.in) != hipSuccess) {
+            asr_pipeline_destroy(p);
+            *out = nullptr;
+            return ASR_ERR_OOM;
+        }
+        p->stage.push_back(b);
+    }
+    return ASR_OK;
+}
+
+int asr_pipeline_get_coalesce(asr_pipeline_t* p, int* group, int* batch, int* column) {
+    if (!p) return ASR_ERR_ARG;
+    if (group) *group = p->cg;
+    if (batch) *batch = p->cg > 1 ? p->Bo : p->cfg.B;
+    if (column) *column = p->cg > 1 ? p->ocol : 0;
+    return ASR_OK;
+}
+
 int asr_pipeline_pending(asr_pipeline_t* p, int* n) {
     if (!p || !n) return ASR_ERR_ARG;
-    *n = (int)(p->submitted - p->collected);
+    *n = p->cg > 1 ? (int)p->opend.size() : (int)(p->submitted - p->collected);
     return ASR_OK;
 }
 

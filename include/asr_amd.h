@@ -388,6 +388,24 @@ int asr_pipeline_submit(asr_pipeline_t* p, const float* d_x);
 int asr_pipeline_collect(asr_pipeline_t* p, int32_t* h_labels, int max_len, int32_t* h_lengths,
                          double* h_logp, float* decode_ms);
 int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
+/* Dynamic batching: a pipeline whose submits carry cfg->B utterances each
+ * and whose launches carry group * cfg->B — `group` consecutive submits are
+ * copied side by side into one batch (time-major [T][group * B][in]) and go
+ * through one production and one decode; asr_pipeline_collect returns each
+ * submit's B rows in submission order.  Collecting a submit whose batch is
+ * not complete queues that batch with zero features in the missing columns
+ * (their rows are decoded and dropped).  The results are the per-submit
+ * pipeline's bits (every utterance is independent).  group = 1 is
+ * asr_pipeline_create.  ASR_ERR_UNSUPPORTED for schedules whose input
+ * projection does not run on the batch's production stream.  (The
+ * reference decodes one batch per call: CTCBeamSearch.cu:262-312.) */
+int asr_pipeline_create_coalesced(const asr_pipeline_config* cfg, int group, const float* d_W_ih,
+                                  const float* d_W_hh, const float* d_b_ih, const float* d_b_hh,
+                                  const float* d_W_out, const float* d_b_out, asr_pipeline_t** out);
+/* group, utterances per submit, and the column (0 .. group - 1) of the
+ * submit collected last inside its batch (asr_pipeline_peek_emissions then
+ * returns the whole batch's [T][group * B][V] emissions). */
+int asr_pipeline_get_coalesce(asr_pipeline_t* p, int* group, int* batch, int* column);
 /* The schedule chosen: mode (0 CU groups for small batches, 1 chip-filling
  * batches, 2 CU groups for H > 256), decodes in flight, production streams,
  * CUs per decode group / decode partition, and the decoder's waves per

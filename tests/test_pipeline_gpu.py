@@ -491,3 +491,46 @@ def test_pipeline_latches_dense_arith():
         q.close()
     finally:
         asr.set_dense_arith(asr.DENSE_SPLIT_BF16)
+
+
+@pytest.mark.parametrize("group,B,n,interleave", [(4, 64, 10, False), (2, 256, 5, False), (3, 96, 7, True)])
+def test_pipeline_coalesced_matches_sequential(group, B, n, interleave):
+    """Dynamic batching (asr_pipeline_create_coalesced): `group` submits of B
+    utterances run as one chip-filling batch of group * B; every submit's
+    results are the sequential fused production + decode of its own B
+    utterances, bit for bit and in submission order, with a partial batch (n
+    not a multiple of group, or collects interleaved with submits) completed
+    by zero-feature padding; peek_emissions returns the submit's own
+    columns, the bytes model_emissions computes for it alone."""
+    T, inp, H, V, beam = 41, 48, 64, 29, 30
+    W = _weights(inp, H, V, seed=group)
+    rng = np.random.default_rng(group + B)
+    xs = [asr.DeviceMatrix.from_numpy(rng.uniform(-1, 1, (T * B, inp)).astype(np.float32)) for _ in range(n)]
+    pl = asr.Pipeline(T, B, inp, H, V, beam, W, coalesce=group)
+    d = pl.describe()
+    assert d["coalesce"] == group and d["mode"] == "chip-filling batches" and d["fused_emission"], d
+    got, ems = [], []
+
+    def take():
+        lab, ln, lp, ms = pl.collect()
+        got.append(([lab[b, :ln[b]].tolist() for b in range(B)], lp.copy()))
+        ems.append(pl.peek_emissions())
+
+    for i, x in enumerate(xs):
+        pl.submit(x)
+        if interleave and i % 3 == 1:
+            take()
+    while pl.pending():
+        take()
+    pl.close()
+    assert len(got) == n
+    asr.rnn_set_recurrence(asr.RNN_RECUR_MFMA)
+    try:
+        for i, x in enumerate(xs):
+            ref = _sequential(x, W, T, B, inp, H, V, beam, asr.RNN_RECUR_MFMA, fused=True)
+            assert got[i][0] == ref[0] and np.array_equal(got[i][1], ref[1]), f"submit {i}"
+            em = asr.DeviceMatrix(T * B, V)
+            asr.model_emissions(x, W, T, B, em, True, recurrence=d["recurrence"])
+            assert np.array_equal(em.toCpu().reshape(T, B, V), ems[i]), f"submit {i}: emissions"
+    finally:
+        asr.rnn_set_recurrence(asr.RNN_RECUR_AUTO)
