@@ -595,8 +595,8 @@ def main():
                          "0 = auto: 1024 when B is a larger multiple of it on the split-bf16 arithmetic)")
     ap.add_argument("--coalesce", type=int, default=0,
                     help="dynamic batching in the native pipeline (asr_pipeline_create_coalesced): this many "
-                         "consecutive submits run as one batch (1 = off; 0 = auto: submits of fewer than 128 "
-                         "utterances in launches of ~640 (C2: 10), else 1)")
+                         "consecutive submits run as one batch (1 = off; 0 = auto: submits under 512 utterances "
+                         "in launches of 512-640 (C2: 10, 256 per GPU: 2), else 1)")
     ap.add_argument("--py-pipeline", action="store_true",
                     help="the round-2 Python orchestration over torch streams instead of the library's "
                          "native pipeline (asr_pipeline_*); implied by its Python-only knobs")
@@ -1192,12 +1192,14 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
         del xh
     else:
         xs = [d_x]
-    # dynamic batching: C2's 64-utterance steps as launches of 640 (run r6cc,
-    # 20 / 5: 1 / 4 / 10 / 20 submits per launch 66.0 / 104.7 / 113.0 / 82.6 M
-    # frames/s; 256 per GPU 1 / 2 / 4: 221.1 / 232.4 / 213.8 M, 512 per GPU 1 / 2:
-    # 303.5 / 266.6 M — larger batches already fill the chip, and fewer,
-    # larger batches lengthen the fill and the drain)
-    cg = args.coalesce if args.coalesce > 0 else (min(10, max(1, 640 // Bp)) if Bp < 128 else 1)
+    # dynamic batching: submits under 512 utterances as launches of 512-640
+    # (runs r6cc / r6dd, 20 / 5, frames/s: C2's 64 per submit at 1 / 4 / 5 /
+    # 10 / 20 per launch 66.0 / 104.7 / 107.7 / 113.0-115.1 / 82.6 M; 128 per
+    # GPU 1 / 4: 133.8 / 204.6 M; 256 per GPU 1 / 2 / 4: 218.8-224.2 /
+    # 232.4-236.4 / 213.8 M; 512 per GPU 1 / 2: 303.5 / 266.6 M — fewer,
+    # larger batches lengthen the fill and the drain once a batch fills the chip)
+    cg = args.coalesce if args.coalesce > 0 else (
+        min(10, max(1, (640 if Bp < 128 else 512) // Bp)) if Bp < 512 else 1)
     pl = asr.Pipeline(T, Bp, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
                       inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus,
                       segments=args.segments, coalesce=cg)
