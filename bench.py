@@ -1198,11 +1198,20 @@ def main_native(args, asr, rank, world, first, GB, B, T, In, H, V, beam, strong,
     # GPU 1 / 4: 133.8 / 204.6 M; 256 per GPU 1 / 2 / 4: 218.8-224.2 /
     # 232.4-236.4 / 213.8 M; 512 per GPU 1 / 2: 303.5 / 266.6 M — fewer,
     # larger batches lengthen the fill and the drain once a batch fills the chip)
-    cg = args.coalesce if args.coalesce > 0 else (
-        min(10, max(1, (640 if Bp < 128 else 512) // Bp)) if Bp < 512 else 1)
-    pl = asr.Pipeline(T, Bp, In, H, V, beam, [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout],
-                      inflight=args.inflight, prod_streams=args.prod_streams, decode_cus=dcus,
-                      segments=args.segments, coalesce=cg)
+    # (measured for the fused H <= 256, V <= 32, beam <= 56 shapes only: C5,
+    # BL and C3's beam 100 keep one submit per launch)
+    small = H <= 256 and V <= 32 and beam <= 56 and Bp < 512
+    cg = args.coalesce if args.coalesce > 0 else (min(10, max(1, (640 if Bp < 128 else 512) // Bp)) if small else 1)
+    pw = [d_wih, d_whh, d_bih, d_bhh, d_wout, d_bout]
+    try:
+        pl = asr.Pipeline(T, Bp, In, H, V, beam, pw, inflight=args.inflight, prod_streams=args.prod_streams,
+                          decode_cus=dcus, segments=args.segments, coalesce=cg)
+    except asr.AsrError:
+        if cg == 1 or args.coalesce > 0:
+            raise
+        cg = 1   # a schedule the library does not coalesce
+        pl = asr.Pipeline(T, Bp, In, H, V, beam, pw, inflight=args.inflight, prod_streams=args.prod_streams,
+                          decode_cus=dcus, segments=args.segments)
     desc = pl.describe()
     if desc["mode"] == asr.PIPELINE_MODES[1] and H <= 256:
         # the pipeline's MFMA recurrence for chip-filling batches, also for
