@@ -9,7 +9,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeou
 rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 400 python bench.py > $O/bench_c4.json 2> $O/bench_c4.err || { tail $O/bench_c4.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench_c4.json'));r=d['roofline'];print('c4', d['value'], d['parity']['match'], d['cpu_baseline']['value'], r['frac'], r.get('serialized',{}).get('ms_per_launch'), r.get('serialized',{}).get('frac'))"
-for a in "c5:--config C5 --no-cpu-baseline" "c2:--config C2" "g256:--batch 256 --no-cpu-baseline"; do
+for a in "c5:--config C5 --no-cpu-baseline" "c2:--config C2" "g256:--batch 256 --no-cpu-baseline" "c3:--config C3 --no-cpu-baseline --no-serialized" "bl:--config BL --no-cpu-baseline --no-serialized"; do
   n=${a%%:*}; args=${a#*:}
   timeout -k 10 300 python bench.py $args > $O/bench_$n.json 2> $O/bench_$n.err || { tail $O/bench_$n.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/bench_$n.json'));print('$n', d['value'], (d.get('parity') or {}).get('match'))"
