@@ -1222,8 +1222,10 @@ int asr_pipeline_create_coalesced(const asr_pipeline_config* cfg, int group, con
     if (int rc = asr_pipeline_create(&c, W_ih, W_hh, b_ih, b_hh, W_out, b_out, out)) return rc;
     asr_pipeline* p = *out;
     // the caller's features are copied onto the production stream that reads
-    // them: schedules whose input projection runs elsewhere are not coalesced
-    if (p->split || p->G > 1 || p->grows > 0) {
+    // them: schedules whose input projection runs elsewhere are not coalesced;
+    // nor are the unfused productions, whose kernels are chosen by the batch
+    // shape (the fused one's bits do not depend on it)
+    if (p->split || p->G > 1 || p->grows > 0 || !p->fuse || p->mode != SHARED) {
         asr_pipeline_destroy(p);
         *out = nullptr;
         return ASR_ERR_UNSUPPORTED;

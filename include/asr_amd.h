@@ -396,8 +396,10 @@ int asr_pipeline_pending(asr_pipeline_t* p, int* n_uncollected);
  * not complete queues that batch with zero features in the missing columns
  * (their rows are decoded and dropped).  The results are the per-submit
  * pipeline's bits (every utterance is independent).  group = 1 is
- * asr_pipeline_create.  ASR_ERR_UNSUPPORTED for schedules whose input
- * projection does not run on the batch's production stream.  (The
+ * asr_pipeline_create.  ASR_ERR_UNSUPPORTED unless the batch of
+ * group * B runs the chip-filling schedule with the fused production
+ * (H <= 256, V <= 32: the production whose bits do not depend on the batch
+ * shape, its input projection on the batch's production stream).  (The
  * reference decodes one batch per call: CTCBeamSearch.cu:262-312.) */
 int asr_pipeline_create_coalesced(const asr_pipeline_config* cfg, int group, const float* d_W_ih,
                                   const float* d_W_hh, const float* d_b_ih, const float* d_b_hh,

@@ -33,12 +33,13 @@ def test_inflight_and_split_production_match_sequential():
     (recurrence, then the emission GEMM), the same bits."""
     groups = {"ASR_PIPELINE_MODE": "0"}
     seq = _bench("--no-pipeline")
+    one = ("--coalesce", "1")   # 64-utterance batches (no dynamic batching)
     runs = {
-        "packed": _bench("--packed"),   # 4-wave decode workgroups two to a CU, 5 batches in flight
-        "d1": _bench("--inflight", "1", env=groups),
-        "d3_split_all": _bench("--inflight", "3", env=groups),   # auto: production split, GEMMs on all CUs
+        "packed": _bench("--packed", *one),   # 4-wave decode workgroups two to a CU, 5 batches in flight
+        "d1": _bench("--inflight", "1", *one, env=groups),
+        "d3_split_all": _bench("--inflight", "3", *one, env=groups),   # auto: production split, GEMMs on all CUs
         "d2_unsplit_graph": _bench("--inflight", "2", "--prod-split", "off", "--graph-production", "on",
-                                   "--prod-streams", "2"),
+                                   "--prod-streams", "2", *one),
     }
     assert seq["gather"]["utterances"] == 64
     for name, r in runs.items():
@@ -53,12 +54,16 @@ def test_c2_chip_filling_schedule_independent():
     schedule: one-wave decodes, 10 in flight, fused production) gathers the
     same digest at 1, 3 and the default decodes in flight and with the
     production in one T-segment — placement and overlap never change a bit."""
-    base = _bench()
+    base = _bench("--coalesce", "1")
     assert base["config"]["inflight_decodes"] == 10 and base["config"]["decode_waves"] == -1, base["config"]
     assert base["config"]["fused_emission"] is True
     for args in (("--inflight", "1"), ("--inflight", "3"), ("--segments", "1")):
-        r = _bench(*args)
+        r = _bench(*args, "--coalesce", "1")
         assert r["gather"] == base["gather"], args
+    # the default: dynamic batching (ten 64-utterance submits per launch), the same bits
+    co = _bench()
+    assert co["config"]["coalesce"] == 10, co["config"]
+    assert co["gather"] == base["gather"]
 
 
 def test_c4_self_launched_ranks_match_one_rank():
